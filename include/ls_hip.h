@@ -1,0 +1,211 @@
+/*
+ * ls_hip.h -- C-ABI of the MI355X (gfx950) kernel library libls_hip.so for the
+ * LatentSync inference denoising hot path.
+ *
+ * The reference has no FFI on this path: its swap points are
+ * the duck-typed Python objects injected into LipsyncPipeline.__init__
+ * (latentsync/pipelines/lipsync_pipeline.py:49-124).  This library sits UNDER
+ * those objects; the host package latentsync_amd binds it with ctypes.  Every
+ * entry point below names the reference interface whose arithmetic it replaces.
+ *
+ * Conventions
+ *   - All tensors are caller-allocated device buffers (plain pointers); no entry
+ *     point allocates, frees or synchronises, so every call can be captured into
+ *     a hipGraph.  `stream` is a hipStream_t (NULL = default stream).
+ *   - Activations are "pixel-major" (NHWC): frames are folded into the image
+ *     index exactly like InflatedConv3d's "b c f h w -> (b f) c h w"
+ *     (latentsync/models/resnet.py:10-18); element (img, y, x, c) lives at
+ *     ((img*H + y)*W + x)*ld + c.  Storage type is bf16 (uint16_t bit pattern)
+ *     unless a field says fp32.
+ *   - Return value: 0 = LS_OK, otherwise an ls_status; ls_last_error() returns
+ *     a thread-local message for the last failure.
+ */
+#ifndef LS_HIP_H
+#define LS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LS_ABI_VERSION 1
+
+typedef enum {
+  LS_OK = 0,
+  LS_ERR_INVALID = 1,  /* bad shape / alignment / unsupported combination */
+  LS_ERR_LAUNCH = 2,   /* hipLaunchKernel / hipGetLastError failure       */
+  LS_ERR_WORKSPACE = 3 /* workspace missing or too small                   */
+} ls_status;
+
+enum { LS_ACT_NONE = 0, LS_ACT_GEGLU = 1, LS_ACT_GELU = 2, LS_ACT_SILU = 3 };
+
+/*
+ * Fused implicit-GEMM convolution / linear layer on bf16 MFMA
+ * (v_mfma_f32_16x16x32_bf16), fp32 accumulate.
+ *
+ *   Y[m, n] = epilogue( sum_k A[m, k] * Wp[n, k] )
+ *
+ * A is never materialised: row m is an output pixel (img, yo, xo); column
+ * k = tap*Cin + ci reads input channel ci of the tap's source pixel, from x1
+ * (ci < C1) or x2 (ci >= C1, the fused torch.cat of the up blocks,
+ * unet_blocks.py:624,745).  Optional prologue per element (fused GroupNorm
+ * apply + SiLU of ResnetBlock3D, resnet.py:185-186 / 207-213):
+ *   a = x * aff_scale[s, ci] + aff_shift[s, ci]; if (silu_in) a = silu(a)
+ * with s = img / imgs_per_sample.  Zero padding is applied after the prologue.
+ * ksize 1 = linear / 1x1 conv (Transformer proj_in/out, q/k/v/out, FF, shortcut);
+ * ksize 3 = InflatedConv3d 3x3 (conv1/2, conv_in/out, samplers).
+ * stride 2 + pad 1 = Downsample3D (resnet.py:89), stride 2 + pad 0 = the SD-VAE
+ * downsampler after F.pad(0,1,0,1); upsample = nearest x2 fused into the
+ * gather (Upsample3D, resnet.py:53-73).
+ *
+ * Wp is the packed weight [N][K]: K = ksize*ksize*Cin rounded up to 64, tap-major
+ * (see latentsync_amd/packing.py).  Epilogue, in this order:
+ *   v = acc + bias[n] + rowvec[(m / rows_per_vec) * rowvec_ld + n]  (temb add, resnet.py:190-205)
+ *   v = (v + res[m, n]) * out_scale                      (residual, resnet.py:221)
+ *   act: GEGLU pairs packed columns (32b+i, 32b+16+i) -> out col 16b+i,
+ *        out = h * gelu_erf(g) (diffusers GEGLU); GELU (whisper MLP); SiLU.
+ * split_k > 1 needs `workspace` of split_k*M*N fp32 (ls_conv_workspace_bytes).
+ */
+typedef struct {
+  const uint16_t* x1; const uint16_t* x2;
+  int32_t C1, C2;            /* channels read from x1 / x2 (C2 = 0: no concat) */
+  int32_t ld1, ld2;          /* pixel pitch (elements) of x1 / x2             */
+  int32_t n_img, H, W;       /* input images / resolution (ksize 1: H=1, W=rows) */
+  int32_t Ho, Wo;            /* output resolution                              */
+  int32_t ksize, stride, pad, upsample;
+  const float* aff_scale; const float* aff_shift; int32_t imgs_per_sample; int32_t silu_in;
+  const uint16_t* w; int32_t K; int32_t N;
+  const float* bias;
+  const float* rowvec; int32_t rows_per_vec; int32_t rowvec_ld; /* rowvec_ld 0 = N */
+  const uint16_t* res; int32_t ldr; float out_scale;
+  int32_t act;
+  void* y; int32_t ldy; int32_t y_f32;
+  int32_t split_k;           /* 0 = choose automatically                       */
+  void* workspace; size_t workspace_bytes;
+} ls_conv_desc;
+
+int ls_conv2d(const ls_conv_desc* d, void* stream);
+size_t ls_conv_workspace_bytes(const ls_conv_desc* d);
+
+/*
+ * GroupNorm statistics -> per-(sample, channel) affine for the consumer's
+ * prologue.  Replaces nn.GroupNorm of ResnetBlock3D (5-D: stats span all frames
+ * of a sample, resnet.py:140,164; unet.py:236), Transformer3DModel.norm and
+ * TemporalTransformer3DModel.norm (4-D per frame, attention.py:51,
+ * motion_module.py:101) and the SD-VAE GroupNorms.
+ * Input: n_samples * pix_per_sample pixels of C = C1 + C2 channels (x2 = concat).
+ * Output: scale[s, c] = gamma[c] * rstd[s, g]; shift[s, c] = beta[c] - mean[s, g] * scale.
+ * workspace >= ls_groupnorm_workspace_bytes().
+ */
+int ls_groupnorm(const uint16_t* x1, const uint16_t* x2, int32_t C1, int32_t C2, int32_t n_samples,
+                 int64_t pix_per_sample, int32_t groups, float eps, const float* gamma, const float* beta,
+                 float* scale, float* shift, void* workspace, size_t workspace_bytes, void* stream);
+size_t ls_groupnorm_workspace_bytes(int32_t n_samples, int32_t groups);
+
+/* Materialised GroupNorm(+SiLU) apply (used where the consumer is not a GEMM). */
+int ls_affine_act(const uint16_t* x, int64_t n_pix, int32_t C, int64_t pix_per_sample, const float* scale,
+                  const float* shift, int32_t silu, uint16_t* y, void* stream);
+
+/*
+ * LayerNorm over the last dim (nn.LayerNorm of BasicTransformerBlock
+ * attention.py:145,157,172 and TemporalTransformerBlock motion_module.py:195,201;
+ * whisper LayerNorm model.py:29-31).  Optional fused temporal positional
+ * encoding add (VersatileAttention pos_encoder, motion_module.py:267-268):
+ *   y[r, c] += pe[(r / pe_rows_per_frame) % pe_frames, c]   (pe fp32 [len][C]).
+ */
+int ls_layernorm(const uint16_t* x, int64_t rows, int32_t C, float eps, const float* gamma, const float* beta,
+                 const float* pe, int32_t pe_rows_per_frame, int32_t pe_frames, uint16_t* y, void* stream);
+
+/*
+ * Multi-head attention softmax(Q K^T * scale) V on MFMA with LDS-staged K/V
+ * tiles (F.scaled_dot_product_attention of Attention.forward attention.py:271,
+ * VersatileAttention motion_module.py:300, whisper qkv_attention model.py:88-100,
+ * SD-VAE mid attention).  Element (b, h, i, d) of T in {q,k,v,o} is at
+ *   T + (b / z2)*T_sb1 + (b % z2)*T_sb2 + i*T_si + h*T_sh + d
+ * so spatial (rows = tokens), temporal ("(b f) s c -> (b s) f c") and audio
+ * cross-attention (Nk = 50) are strided views of the projection outputs.
+ * head_dim <= 512.
+ */
+typedef struct {
+  const uint16_t* q; const uint16_t* k; const uint16_t* v; uint16_t* o;
+  int64_t q_sb1, q_sb2, q_si, q_sh;
+  int64_t k_sb1, k_sb2, k_si, k_sh;
+  int64_t v_sb1, v_sb2, v_si, v_sh;
+  int64_t o_sb1, o_sb2, o_si, o_sh;
+  int32_t batch, z2, heads, nq, nk, head_dim;
+  float scale;
+} ls_attn_desc;
+
+int ls_attention(const ls_attn_desc* d, void* stream);
+
+/*
+ * Small-M linear in fp32: y[m, n] = sum_k act(x[m, k]) * W[n, k] + bias[n]
+ * (x fp32, W bf16 [N][K]); pre-activation SiLU optional.  TimestepEmbedding
+ * (unet.py:382) and the batched time_emb_proj of every ResnetBlock3D
+ * (resnet.py:190-194).
+ */
+int ls_small_linear(const float* x, int32_t M, int32_t K, const uint16_t* w, const float* bias, int32_t N,
+                    int32_t silu_in, float* y, void* stream);
+
+/* diffusers Timesteps(320, flip_sin_to_cos, shift) (unet.py:95,376): t read from
+ * timesteps[*step] (device int32 array + device step index), out fp32 [B][dim]. */
+int ls_timestep_embed(const int32_t* timesteps, const int32_t* step, int32_t B, int32_t dim, int32_t flip,
+                      float shift, float* out, void* stream);
+
+/*
+ * CFG combine + DDIMScheduler.step (eta = 0) fused, then re-packs the next UNet
+ * input (lipsync_pipeline.py:540-562).  eps: UNet output bf16 NHWC [Bu*P][ld_eps]
+ * (4 used channels); lat fp32 [P][4] updated in place; coef fp32 table
+ * [n_steps][4] = {sqrt(a_t), sqrt(1-a_t), sqrt(a_prev), sqrt(1-a_prev)} read at
+ * *step; then *step += 1 (single thread).  When guidance > 1 the batch halves are
+ * (uncond, audio).  unet_in (bf16 NHWC [Bu*P][ld_in]) receives the new latents in
+ * channels 0..3 of every batch copy.
+ */
+int ls_ddim_cfg_step(const uint16_t* eps, int32_t ld_eps, int32_t Bu, int64_t P, float guidance, float* lat,
+                     const float* coef, int32_t* step, uint16_t* unet_in, int32_t ld_in, void* stream);
+
+/* Pixel prep (ImageProcessor.preprocess_fixed_mask_image image_processor.py:145-152):
+ * faces uint8 NCHW [F][3][R][R]; mask fp32 [R][R] (1 = keep);
+ * pix / masked bf16 NHWC [F][R][R][ld] (channels 3..ld-1 zeroed). */
+int ls_prep_pixels(const uint8_t* faces, int32_t F, int32_t R, const float* mask, uint16_t* pix, uint16_t* masked,
+                   int32_t ld, void* stream);
+
+/* DiagonalGaussianDistribution.sample + (z - shift) * scaling (lipsync_pipeline.py:296-297):
+ * moments fp32 NHWC [P][ld_m] (mean = ch 0..3, logvar = ch 4..7), eps fp32 [P][4];
+ * writes bf16 into dst[P][ld_dst] at channel offset c_off. */
+int ls_vae_sample(const float* moments, int32_t ld_m, const float* eps, int64_t P, float scaling, float shift,
+                  uint16_t* dst, int32_t ld_dst, int32_t c_off, void* stream);
+
+/* Builds the constant channels of the UNet input for a window
+ * (lipsync_pipeline.py:517-549): ch 4 = nearest-resized keep-mask (prepare_mask_latents
+ * :290), ch 5..8 masked-image latents, ch 9..12 reference latents (both already
+ * written by ls_vae_sample into `cond` [P][16]); replicated into Bu copies of
+ * unet_in [Bu][P][ld_in] together with the initial latents lat fp32 [P][4]. */
+int ls_pack_unet_input(const float* lat, const uint16_t* cond, const float* mask, int32_t F, int32_t R, int32_t h,
+                       int32_t Bu, uint16_t* unet_in, int32_t ld_in, void* stream);
+
+/* decode_latents prep (lipsync_pipeline.py:146-147): z = lat / scaling + shift,
+ * lat fp32 [P][4] -> bf16 NHWC [P][ld]. */
+int ls_scale_latents(const float* lat, int64_t P, float inv_scaling, float shift, uint16_t* z, int32_t ld,
+                     void* stream);
+
+/* paste_surrounding_pixels_back + pixel_values_to_images (lipsync_pipeline.py:327-341):
+ * out = dec * (1 - keep) + pix * keep; dec / pix bf16 NHWC [F][R][R][ld*];
+ * out_nchw fp32 [F][3][R][R] (may be NULL), out_u8 uint8 [F][R][R][3] (may be NULL). */
+int ls_paste_back(const uint16_t* dec, int32_t ld_dec, const uint16_t* pix, int32_t ld_pix, const float* mask,
+                  int32_t F, int32_t R, float* out_nchw, uint8_t* out_u8, void* stream);
+
+/* y[r, c] = x[r, c] + table[r % table_rows, c] (table fp32 [table_rows][C]): the
+ * whisper positional-embedding add (whisper/model.py:155). */
+int ls_add_rows(const uint16_t* x, int64_t rows, int32_t C, int32_t ldx, const float* table, int32_t table_rows,
+                uint16_t* y, int32_t ldy, void* stream);
+
+int ls_abi_version(void);
+const char* ls_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LS_HIP_H */

@@ -1,0 +1,102 @@
+"""ctypes binding of libls_hip.so (include/ls_hip.h).
+
+This is the only door from the host package to the kernels.  There is no
+fallback: if the library is missing or was built for another ABI, importing
+the product path raises immediately (loud failure is part of the parity
+contract -- a silent CPU/eager fallback would void every GPU parity claim).
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("LS_HIP_LIB", os.path.join(HERE, "libls_hip.so"))
+ABI_VERSION = 1
+
+c_u16p = C.c_void_p
+c_vp = C.c_void_p
+
+
+class ConvDesc(C.Structure):
+    _fields_ = [
+        ("x1", c_vp), ("x2", c_vp),
+        ("C1", C.c_int32), ("C2", C.c_int32),
+        ("ld1", C.c_int32), ("ld2", C.c_int32),
+        ("n_img", C.c_int32), ("H", C.c_int32), ("W", C.c_int32),
+        ("Ho", C.c_int32), ("Wo", C.c_int32),
+        ("ksize", C.c_int32), ("stride", C.c_int32), ("pad", C.c_int32), ("upsample", C.c_int32),
+        ("aff_scale", c_vp), ("aff_shift", c_vp), ("imgs_per_sample", C.c_int32), ("silu_in", C.c_int32),
+        ("w", c_vp), ("K", C.c_int32), ("N", C.c_int32),
+        ("bias", c_vp),
+        ("rowvec", c_vp), ("rows_per_vec", C.c_int32), ("rowvec_ld", C.c_int32),
+        ("res", c_vp), ("ldr", C.c_int32), ("out_scale", C.c_float),
+        ("act", C.c_int32),
+        ("y", c_vp), ("ldy", C.c_int32), ("y_f32", C.c_int32),
+        ("split_k", C.c_int32),
+        ("workspace", c_vp), ("workspace_bytes", C.c_size_t),
+    ]
+
+
+class AttnDesc(C.Structure):
+    _fields_ = [("q", c_vp), ("k", c_vp), ("v", c_vp), ("o", c_vp)] + [
+        (f"{t}_{s}", C.c_int64) for t in "qkvo" for s in ("sb1", "sb2", "si", "sh")
+    ] + [
+        ("batch", C.c_int32), ("z2", C.c_int32), ("heads", C.c_int32), ("nq", C.c_int32),
+        ("nk", C.c_int32), ("head_dim", C.c_int32), ("scale", C.c_float),
+    ]
+
+
+_SIGS = {
+    "ls_abi_version": (C.c_int, []),
+    "ls_last_error": (C.c_char_p, []),
+    "ls_conv2d": (C.c_int, [C.POINTER(ConvDesc), c_vp]),
+    "ls_conv_workspace_bytes": (C.c_size_t, [C.POINTER(ConvDesc)]),
+    "ls_groupnorm": (C.c_int, [c_vp, c_vp, C.c_int32, C.c_int32, C.c_int32, C.c_int64, C.c_int32, C.c_float,
+                               c_vp, c_vp, c_vp, c_vp, c_vp, C.c_size_t, c_vp]),
+    "ls_groupnorm_workspace_bytes": (C.c_size_t, [C.c_int32, C.c_int32]),
+    "ls_affine_act": (C.c_int, [c_vp, C.c_int64, C.c_int32, C.c_int64, c_vp, c_vp, C.c_int32, c_vp, c_vp]),
+    "ls_layernorm": (C.c_int, [c_vp, C.c_int64, C.c_int32, C.c_float, c_vp, c_vp, c_vp, C.c_int32, C.c_int32,
+                               c_vp, c_vp]),
+    "ls_attention": (C.c_int, [C.POINTER(AttnDesc), c_vp]),
+    "ls_small_linear": (C.c_int, [c_vp, C.c_int32, C.c_int32, c_vp, c_vp, C.c_int32, C.c_int32, c_vp, c_vp]),
+    "ls_timestep_embed": (C.c_int, [c_vp, c_vp, C.c_int32, C.c_int32, C.c_int32, C.c_float, c_vp, c_vp]),
+    "ls_ddim_cfg_step": (C.c_int, [c_vp, C.c_int32, C.c_int32, C.c_int64, C.c_float, c_vp, c_vp, c_vp, c_vp,
+                                   C.c_int32, c_vp]),
+    "ls_prep_pixels": (C.c_int, [c_vp, C.c_int32, C.c_int32, c_vp, c_vp, c_vp, C.c_int32, c_vp]),
+    "ls_vae_sample": (C.c_int, [c_vp, C.c_int32, c_vp, C.c_int64, C.c_float, C.c_float, c_vp, C.c_int32,
+                                C.c_int32, c_vp]),
+    "ls_pack_unet_input": (C.c_int, [c_vp, c_vp, c_vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, c_vp,
+                                     C.c_int32, c_vp]),
+    "ls_scale_latents": (C.c_int, [c_vp, C.c_int64, C.c_float, C.c_float, c_vp, C.c_int32, c_vp]),
+    "ls_paste_back": (C.c_int, [c_vp, C.c_int32, c_vp, C.c_int32, c_vp, C.c_int32, C.c_int32, c_vp, c_vp, c_vp]),
+    "ls_add_rows": (C.c_int, [c_vp, C.c_int64, C.c_int32, C.c_int32, c_vp, C.c_int32, c_vp, C.c_int32, c_vp]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+_lib = None
+
+
+def load(path: str = None):
+    """Load (once) and type the library.  Raises if it is missing or stale."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or LIB_PATH
+    if not os.path.exists(path):
+        raise RuntimeError(f"libls_hip.so not found at {path}: run `python -m latentsync_amd.build` "
+                           "(the HIP library is required; there is no fallback path)")
+    lib = C.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.ls_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"libls_hip.so ABI {lib.ls_abi_version()} != {ABI_VERSION}; rebuild it")
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = _lib.ls_last_error().decode() if _lib is not None else ""
+        raise RuntimeError(f"{what} failed (status {rc}): {msg}")

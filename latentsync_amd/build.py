@@ -1,0 +1,61 @@
+"""Builds libls_hip.so (all HIP kernels + the C-ABI) in-tree for gfx950.
+
+    python -m latentsync_amd.build        # incremental
+Compiles each csrc/*.hip with hipcc --offload-arch=gfx950 -O3 -fPIC into
+build/ objects and links latentsync_amd/libls_hip.so.  No CUDA, no dual path.
+"""
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+OBJ = os.path.join(REPO, "build", "obj")
+LIB = os.path.join(HERE, "libls_hip.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result", "-munsafe-fp-atomics"]
+
+
+def _deps():
+    hdrs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    hdrs.append(os.path.join(REPO, "include", "ls_hip.h"))
+    return max(os.path.getmtime(h) for h in hdrs)
+
+
+def _compile(src, obj, dep_time):
+    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), dep_time):
+        return obj, None
+    cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        return obj, r.stderr
+    return obj, None
+
+
+def build(verbose=True):
+    os.makedirs(OBJ, exist_ok=True)
+    srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
+    dep_time = _deps()
+    objs = []
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        futs = [ex.submit(_compile, s, os.path.join(OBJ, os.path.basename(s)[:-4] + ".o"), dep_time) for s in srcs]
+        for f in futs:
+            obj, err = f.result()
+            if err:
+                raise RuntimeError(f"hipcc failed for {obj}:\n{err}")
+            objs.append(obj)
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("link failed:\n" + r.stderr)
+        if verbose:
+            print("built", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build()
+    sys.exit(0)

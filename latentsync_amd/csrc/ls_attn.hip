@@ -1,0 +1,204 @@
+// Flash-style multi-head attention for gfx950 (bf16 MFMA 16x16x32, fp32 online
+// softmax).
+//
+// Each wave owns 16 queries of one (batch, head); the waves of a block share the
+// K/V tiles staged in LDS.  The score tile is computed TRANSPOSED, S^T = K Q^T
+// (A = K rows from LDS via ds_read_b128, B = Q^T held in registers), so the
+// accumulator has the key on the register/row axis and the query on the lane.
+// That makes (a) the softmax max/sum per query a 4-register + 2-shuffle
+// reduction, and (b) the probabilities already the B operand of the next MFMA,
+// O^T = V^T P^T, with no LDS round trip: the MFMA's k index is permuted
+// identically on both operands (keys 32c+4h+j and 32c+16+4h+j for lane group h),
+// and V^T comes from the row-major V tile through ds_read_b64_tr_b16.
+#include "ls_common.h"
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+
+namespace ls {
+
+struct AttnArgs {
+  const u16* q; const u16* k; const u16* v; u16* o;
+  long q_sb1, q_sb2, q_si, q_sh;
+  long k_sb1, k_sb2, k_si, k_sh;
+  long v_sb1, v_sb2, v_si, v_sh;
+  long o_sb1, o_sb2, o_si, o_sh;
+  int z2, nq, nk, D;
+  float scale_log2;
+};
+
+template <int DP, int NKF>
+__global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
+  constexpr int KC = DP / 32;   // 32-wide d chunks (QK^T k-steps)
+  constexpr int ND = DP / 16;   // 16-row O^T fragments
+  constexpr int KT = 16 * NKF;  // keys per tile
+  constexpr int PITCH = DP + 8; // LDS row pitch (elements), 16-B aligned
+  extern __shared__ __attribute__((aligned(16))) u16 sm[];
+  u16* Ks = sm;
+  u16* Vs = sm + KT * PITCH;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
+  const int h = blockIdx.y;
+  const int b = blockIdx.z;
+  const long b1 = b / a.z2, b2 = b - b1 * a.z2;
+  const u16* qb = a.q + b1 * a.q_sb1 + b2 * a.q_sb2 + (long)h * a.q_sh;
+  const u16* kb = a.k + b1 * a.k_sb1 + b2 * a.k_sb2 + (long)h * a.k_sh;
+  const u16* vb = a.v + b1 * a.v_sb1 + b2 * a.v_sb2 + (long)h * a.v_sh;
+  u16* ob = a.o + b1 * a.o_sb1 + b2 * a.o_sb2 + (long)h * a.o_sh;
+  const int q0 = (blockIdx.x * nw + wid) * 16;
+  const int lq = lane & 15, lg = lane >> 4;
+
+  // Q^T fragments (B operand): lane holds Q[q0+lq][32kc + 8lg .. +8]
+  bf16x8 qf[KC];
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) {
+    const int d = kc * 32 + lg * 8;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (q0 + lq < a.nq && d < a.D) v = *(const uint4*)(qb + (long)(q0 + lq) * a.q_si + d);
+    qf[kc] = __builtin_bit_cast(bf16x8, v);
+  }
+
+  f32x4 oacc[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) oacc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+
+  const int cpr = DP / 8;  // 16-B chunks per row
+  for (int t0 = 0; t0 < a.nk; t0 += KT) {
+    __syncthreads();
+    for (int i = tid; i < KT * cpr; i += blockDim.x) {
+      const int r = i / cpr, c = (i - r * cpr) * 8;
+      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+      if (t0 + r < a.nk && c < a.D) {
+        kv = *(const uint4*)(kb + (long)(t0 + r) * a.k_si + c);
+        vv = *(const uint4*)(vb + (long)(t0 + r) * a.v_si + c);
+      }
+      *(uint4*)(Ks + r * PITCH + c) = kv;
+      *(uint4*)(Vs + r * PITCH + c) = vv;
+    }
+    __syncthreads();
+
+    // S^T = K Q^T : s[f][r] = score(key t0 + 16f + 4lg + r, query q0 + lq)
+    f32x4 s[NKF];
+#pragma unroll
+    for (int f = 0; f < NKF; ++f) {
+      s[f] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        const bf16x8 kf = __builtin_bit_cast(bf16x8, *(const uint4*)(Ks + (16 * f + lq) * PITCH + kc * 32 + lg * 8));
+        s[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[kc], s[f], 0, 0, 0);
+      }
+    }
+    float mt = -INFINITY;
+#pragma unroll
+    for (int f = 0; f < NKF; ++f)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = t0 + 16 * f + 4 * lg + r;
+        const float x = key < a.nk ? s[f][r] * a.scale_log2 : -INFINITY;
+        s[f][r] = x;
+        mt = fmaxf(mt, x);
+      }
+    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float mn = fmaxf(m, mt);
+    const float alpha = exp2f(m - mn);
+    m = mn;
+    float ps = 0.f;
+#pragma unroll
+    for (int f = 0; f < NKF; ++f)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(s[f][r] - mn);
+        s[f][r] = p;
+        ps += p;
+      }
+    l = l * alpha + ps;
+#pragma unroll
+    for (int i = 0; i < ND; ++i) oacc[i] *= alpha;
+
+    // O^T += V^T P^T over 32-key chunks
+#pragma unroll
+    for (int c = 0; c < NKF / 2; ++c) {
+      bf16x8 pb;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pb[r] = (__bf16)s[2 * c][r];
+        pb[4 + r] = (__bf16)s[2 * c + 1][r];
+      }
+      const int qq = lq >> 2, pp = lq & 3;
+      const u16* va = Vs + (32 * c + 4 * lg + qq) * PITCH + 4 * pp;
+      const u16* vb2 = va + 16 * PITCH;
+#pragma unroll
+      for (int nd = 0; nd < ND; ++nd) {
+        const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4i16*)(va + nd * 16));
+        const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4i16*)(vb2 + nd * 16));
+        const short __attribute__((ext_vector_type(8))) av = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        oacc[nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av), pb, oacc[nd], 0, 0, 0);
+      }
+    }
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  const float inv = 1.f / l;
+  const int q = q0 + lq;
+  if (q < a.nq) {
+    u16* orow = ob + (long)q * a.o_si;
+#pragma unroll
+    for (int nd = 0; nd < ND; ++nd)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int d = nd * 16 + 4 * lg + r;
+        if (d < a.D) orow[d] = f2bf(oacc[nd][r] * inv);
+      }
+  }
+}
+
+template <int DP, int NKF>
+static int launch_attn(const AttnArgs& a, int batch, int heads, hipStream_t s) {
+  const int nwant = cdiv(a.nq, 16);
+  const int nw = std::min(4, nwant);
+  const dim3 grid(cdiv(nwant, nw), heads, batch);
+  const size_t shm = 2 * (size_t)(16 * NKF) * (DP + 8) * sizeof(u16);
+  if (shm > 64 * 1024) {
+    static bool attr_set = false;
+    if (!attr_set) {
+      hipFuncSetAttribute((const void*)attn_kernel<DP, NKF>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+      attr_set = true;
+    }
+  }
+  attn_kernel<DP, NKF><<<grid, nw * 64, shm, s>>>(a);
+  return check_launch("attn_kernel");
+}
+
+}  // namespace ls
+
+using namespace ls;
+
+extern "C" int ls_attention(const ls_attn_desc* d, void* stream) {
+  if (!d || !d->q || !d->k || !d->v || !d->o) return fail(LS_ERR_INVALID, "ls_attention: null pointer");
+  if (d->head_dim % 8 || d->head_dim <= 0 || d->head_dim > 512 || d->nq <= 0 || d->nk <= 0 || d->batch <= 0 ||
+      d->z2 <= 0 || d->heads <= 0)
+    return fail(LS_ERR_INVALID, "ls_attention: bad shape (head_dim % 8 == 0, <= 512)");
+  AttnArgs a;
+  a.q = d->q; a.k = d->k; a.v = d->v; a.o = d->o;
+  a.q_sb1 = d->q_sb1; a.q_sb2 = d->q_sb2; a.q_si = d->q_si; a.q_sh = d->q_sh;
+  a.k_sb1 = d->k_sb1; a.k_sb2 = d->k_sb2; a.k_si = d->k_si; a.k_sh = d->k_sh;
+  a.v_sb1 = d->v_sb1; a.v_sb2 = d->v_sb2; a.v_si = d->v_si; a.v_sh = d->v_sh;
+  a.o_sb1 = d->o_sb1; a.o_sb2 = d->o_sb2; a.o_si = d->o_si; a.o_sh = d->o_sh;
+  a.z2 = d->z2; a.nq = d->nq; a.nk = d->nk; a.D = d->head_dim;
+  a.scale_log2 = d->scale * 1.4426950408889634f;
+  hipStream_t s = (hipStream_t)stream;
+  const bool small = d->nk <= 32;
+  const int D = d->head_dim;
+#define LS_ATTN(DPV)                                                              \
+  return small ? launch_attn<DPV, 2>(a, d->batch, d->heads, s)                    \
+               : launch_attn<DPV, 4>(a, d->batch, d->heads, s);
+  if (D <= 64) { LS_ATTN(64) }
+  if (D <= 96) { LS_ATTN(96) }
+  if (D <= 160) { LS_ATTN(160) }
+  if (D <= 256) { LS_ATTN(256) }
+  LS_ATTN(512)
+#undef LS_ATTN
+}

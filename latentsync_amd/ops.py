@@ -1,0 +1,224 @@
+"""Thin torch-tensor wrappers over the C-ABI (include/ls_hip.h).
+
+Tensors are device buffers owned by the caller (torch caching allocator); the
+wrappers only compute shapes, fill the descriptors and launch on the current
+HIP stream, so every call is capturable in a hipGraph (torch.cuda.CUDAGraph).
+Activations are NHWC bf16: (images, H, W, C) with frames folded into images.
+"""
+import ctypes as C
+import math
+
+import torch
+
+from . import _lib
+from ._lib import check
+
+ACT_NONE, ACT_GEGLU, ACT_GELU, ACT_SILU = 0, 1, 2, 3
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+class Workspace:
+    """Fixed-size per-device scratch (split-K partials, GroupNorm partials).  Never
+    re-allocated after creation so captured graphs keep valid pointers."""
+
+    def __init__(self, device, gemm_bytes=256 << 20, gn_bytes=16 << 20):
+        self.gemm = torch.empty(gemm_bytes, dtype=torch.uint8, device=device)
+        self.gn = torch.empty(gn_bytes, dtype=torch.uint8, device=device)
+
+
+_WS = {}
+
+
+def workspace(device) -> Workspace:
+    key = torch.device(device).index or 0
+    if key not in _WS:
+        _WS[key] = Workspace(device)
+    return _WS[key]
+
+
+class Packed:
+    """A contraction operand ready for ls_conv2d: w bf16 [N][K] (tap-major,
+    K padded to 64), bias fp32 [N] or None."""
+
+    def __init__(self, w, bias, cin, ksize, n_out, geglu=False):
+        self.w, self.bias, self.cin, self.ksize = w, bias, cin, ksize
+        self.N, self.K = w.shape
+        self.n_out = n_out
+        self.geglu = geglu
+
+
+def conv(x, pw: Packed, *, x2=None, aff=None, stride=1, pad=None, upsample=False, out_hw=None, rowvec=None,
+         res=None, out_scale=1.0, act=ACT_NONE, out=None, out_f32=False, split_k=0):
+    """Fused conv/linear.  x (n, H, W, C1) [+ x2 (n, H, W, C2)] -> (n, Ho, Wo, n_out).
+    aff = (scale[S][C], shift[S][C], imgs_per_sample, silu); rowvec = (t[S][ld], rows_per_vec, ld)."""
+    lib = _lib.load()
+    n, H, W, C1 = x.shape
+    C2 = x2.shape[3] if x2 is not None else 0
+    assert C1 + C2 == pw.cin, (C1, C2, pw.cin)
+    ks = pw.ksize
+    if pad is None:
+        pad = 1 if ks == 3 else 0
+    if out_hw is not None:
+        Ho, Wo = out_hw
+    elif ks == 1:
+        Ho, Wo = H, W
+    else:
+        He, We = (2 * H, 2 * W) if upsample else (H, W)
+        Ho, Wo = (He + 2 * pad - 3) // stride + 1, (We + 2 * pad - 3) // stride + 1
+    n_out = pw.n_out if act != ACT_GEGLU else pw.N // 2
+    if out is None:
+        out = torch.empty((n, Ho, Wo, n_out), dtype=torch.float32 if out_f32 else torch.bfloat16, device=x.device)
+    ws = workspace(x.device)
+    d = _lib.ConvDesc()
+    d.x1, d.x2, d.C1, d.C2 = _p(x), _p(x2), C1, C2
+    d.ld1, d.ld2 = C1, C2
+    d.n_img, d.H, d.W, d.Ho, d.Wo = n, H, W, Ho, Wo
+    d.ksize, d.stride, d.pad, d.upsample = ks, stride, pad, int(upsample)
+    if aff is not None:
+        d.aff_scale, d.aff_shift, d.imgs_per_sample, d.silu_in = _p(aff[0]), _p(aff[1]), aff[2], int(aff[3])
+    d.w, d.K, d.N = _p(pw.w), pw.K, pw.N
+    d.bias = _p(pw.bias)
+    if rowvec is not None:
+        d.rowvec, d.rows_per_vec, d.rowvec_ld = _p(rowvec[0]), rowvec[1], rowvec[2]
+    if res is not None:
+        d.res, d.ldr = _p(res), res.shape[-1]
+    d.out_scale = out_scale
+    d.act = act
+    d.y, d.ldy, d.y_f32 = _p(out), out.shape[-1], int(out.dtype == torch.float32)
+    d.split_k = split_k
+    d.workspace, d.workspace_bytes = _p(ws.gemm), ws.gemm.numel()
+    check(lib.ls_conv2d(C.byref(d), _stream()), "ls_conv2d")
+    return out
+
+
+def linear(x2d, pw: Packed, **kw):
+    """Token-row linear: x2d (rows, C) -> (rows, n_out)."""
+    rows = x2d.shape[0]
+    y = conv(x2d.view(1, 1, rows, x2d.shape[1]), pw, **kw)
+    return y.view(rows, y.shape[-1])
+
+
+def group_norm(x, groups, eps, gamma, beta, n_samples, x2=None):
+    """GroupNorm statistics -> (scale, shift) fp32 [n_samples][C]."""
+    lib = _lib.load()
+    C1 = x.shape[-1]
+    C2 = x2.shape[-1] if x2 is not None else 0
+    pps = x.numel() // C1 // n_samples
+    scale = torch.empty((n_samples, C1 + C2), dtype=torch.float32, device=x.device)
+    shift = torch.empty_like(scale)
+    ws = workspace(x.device)
+    check(lib.ls_groupnorm(_p(x), _p(x2), C1, C2, n_samples, pps, groups, eps, _p(gamma), _p(beta), _p(scale),
+                           _p(shift), _p(ws.gn), ws.gn.numel(), _stream()), "ls_groupnorm")
+    return scale, shift
+
+
+def affine_act(x, scale, shift, n_samples, silu):
+    lib = _lib.load()
+    C_ = x.shape[-1]
+    n_pix = x.numel() // C_
+    y = torch.empty_like(x)
+    check(lib.ls_affine_act(_p(x), n_pix, C_, n_pix // n_samples, _p(scale), _p(shift), int(silu), _p(y), _stream()),
+          "ls_affine_act")
+    return y
+
+
+def layer_norm(x2d, gamma, beta, eps=1e-5, pe=None, pe_rows_per_frame=1, pe_frames=1):
+    lib = _lib.load()
+    rows, C_ = x2d.shape
+    y = torch.empty_like(x2d)
+    check(lib.ls_layernorm(_p(x2d), rows, C_, eps, _p(gamma), _p(beta), _p(pe), pe_rows_per_frame, pe_frames, _p(y),
+                           _stream()), "ls_layernorm")
+    return y
+
+
+def attention(q, k, v, o, *, batch, z2, heads, nq, nk, head_dim, qs, ks, vs, os_, scale=None):
+    """qs/ks/vs/os_ = (sb1, sb2, si, sh) element strides; q/k/v/o base tensors
+    (may be offset views)."""
+    lib = _lib.load()
+    d = _lib.AttnDesc()
+    d.q, d.k, d.v, d.o = _p(q), _p(k), _p(v), _p(o)
+    for t, st in zip("qkvo", (qs, ks, vs, os_)):
+        for name, val in zip(("sb1", "sb2", "si", "sh"), st):
+            setattr(d, f"{t}_{name}", int(val))
+    d.batch, d.z2, d.heads, d.nq, d.nk, d.head_dim = batch, z2, heads, nq, nk, head_dim
+    d.scale = scale if scale is not None else 1.0 / math.sqrt(head_dim)
+    check(lib.ls_attention(C.byref(d), _stream()), "ls_attention")
+    return o
+
+
+def small_linear(x, w, bias, silu_in=False, out=None):
+    lib = _lib.load()
+    M, K = x.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=x.device)
+    check(lib.ls_small_linear(_p(x), M, K, _p(w), _p(bias), N, int(silu_in), _p(out), _stream()), "ls_small_linear")
+    return out
+
+
+def timestep_embed(timesteps_i32, step_i32, B, dim, flip=True, shift=0.0, out=None):
+    lib = _lib.load()
+    if out is None:
+        out = torch.empty((B, dim), dtype=torch.float32, device=timesteps_i32.device)
+    check(lib.ls_timestep_embed(_p(timesteps_i32), _p(step_i32), B, dim, int(flip), float(shift), _p(out), _stream()),
+          "ls_timestep_embed")
+    return out
+
+
+def ddim_cfg_step(eps, Bu, guidance, lat, coef, step, unet_in):
+    lib = _lib.load()
+    P = lat.shape[0]
+    check(lib.ls_ddim_cfg_step(_p(eps), eps.shape[-1], Bu, P, float(guidance), _p(lat), _p(coef), _p(step),
+                               _p(unet_in), unet_in.shape[-1], _stream()), "ls_ddim_cfg_step")
+
+
+def prep_pixels(faces_u8, mask, ld=8):
+    lib = _lib.load()
+    F_, _, R, _ = faces_u8.shape
+    pix = torch.empty((F_, R, R, ld), dtype=torch.bfloat16, device=faces_u8.device)
+    masked = torch.empty_like(pix)
+    check(lib.ls_prep_pixels(_p(faces_u8), F_, R, _p(mask), _p(pix), _p(masked), ld, _stream()), "ls_prep_pixels")
+    return pix, masked
+
+
+def vae_sample(moments, eps, scaling, shift, dst, c_off):
+    lib = _lib.load()
+    P = eps.shape[0]
+    check(lib.ls_vae_sample(_p(moments), moments.shape[-1], _p(eps), P, float(scaling), float(shift), _p(dst),
+                            dst.shape[-1], c_off, _stream()), "ls_vae_sample")
+
+
+def pack_unet_input(lat, cond, mask, F_, R, h, Bu, unet_in):
+    lib = _lib.load()
+    check(lib.ls_pack_unet_input(_p(lat), _p(cond), _p(mask), F_, R, h, Bu, _p(unet_in), unet_in.shape[-1],
+                                 _stream()), "ls_pack_unet_input")
+
+
+def scale_latents(lat, inv_scaling, shift, z):
+    lib = _lib.load()
+    check(lib.ls_scale_latents(_p(lat), lat.shape[0], float(inv_scaling), float(shift), _p(z), z.shape[-1],
+                               _stream()), "ls_scale_latents")
+
+
+def paste_back(dec, pix, mask, out_nchw=None, out_u8=None):
+    lib = _lib.load()
+    F_, R = dec.shape[0], dec.shape[1]
+    check(lib.ls_paste_back(_p(dec), dec.shape[-1], _p(pix), pix.shape[-1], _p(mask), F_, R, _p(out_nchw),
+                            _p(out_u8), _stream()), "ls_paste_back")
+
+
+def add_rows(x2d, table, out=None):
+    lib = _lib.load()
+    rows, C_ = x2d.shape
+    if out is None:
+        out = torch.empty_like(x2d)
+    check(lib.ls_add_rows(_p(x2d), rows, C_, x2d.stride(0), _p(table), table.shape[0], _p(out), out.stride(0),
+                          _stream()), "ls_add_rows")
+    return out

@@ -1,0 +1,62 @@
+"""One-time weight packing from reference-named fp32 state dicts to the layouts
+the kernels consume (done at load / .to(device), never per step).
+
+  conv / linear  W (O, I[, k, k]) -> bf16 [O][K], K = k*k*I8 rounded up to 64,
+                 tap-major (kh, kw, ci), I8 = I rounded up to 8 (zero channels)
+  GEGLU W1       rows [h(4C); g(4C)] interleaved in 16-row blocks so packed
+                 column 32b+i = h_{16b+i}, 32b+16+i = g_{16b+i} (epilogue pairs)
+  fused q|k|v    rows concatenated (self-attention shares one LN output)
+"""
+import torch
+
+
+def _r8(n):
+    return (n + 7) // 8 * 8
+
+
+def _r64(n):
+    return (n + 63) // 64 * 64
+
+
+def pack_weight(w: torch.Tensor, cin_pad: int = None, n_pad: int = None) -> torch.Tensor:
+    """w (O, I) or (O, I, k, k) fp32 -> fp32 (O', K) tap-major, zero padded."""
+    w = w.float()
+    if w.dim() == 2:
+        w = w[:, :, None, None]
+    if w.dim() == 3:  # conv1d (O, I, k) -> 3x3 with the kernel on the middle row
+        O, I, k = w.shape
+        assert k == 3
+        w2 = torch.zeros(O, I, 3, 3, dtype=w.dtype)
+        w2[:, :, 1, :] = w
+        w = w2
+    O, I, kh, kw = w.shape
+    ip = cin_pad or _r8(I)
+    if ip != I:
+        w = torch.cat([w, torch.zeros(O, ip - I, kh, kw, dtype=w.dtype)], 1)
+    w = w.permute(0, 2, 3, 1).reshape(O, kh * kw * ip)
+    K = _r64(w.shape[1])
+    if K != w.shape[1]:
+        w = torch.cat([w, torch.zeros(O, K - w.shape[1], dtype=w.dtype)], 1)
+    if n_pad and n_pad > O:
+        w = torch.cat([w, torch.zeros(n_pad - O, K, dtype=w.dtype)], 0)
+    return w
+
+
+def pad_bias(b, n_pad=None):
+    if b is None:
+        return None
+    b = b.float()
+    if n_pad and n_pad > b.shape[0]:
+        b = torch.cat([b, torch.zeros(n_pad - b.shape[0])])
+    return b
+
+
+def geglu_interleave(w1: torch.Tensor, b1: torch.Tensor):
+    """w1 (8C, C) = [h; g] -> rows interleaved in 16-blocks; b1 likewise."""
+    n2 = w1.shape[0] // 2
+    assert n2 % 16 == 0
+    h, g = w1[:n2], w1[n2:]
+    w = torch.stack([h.reshape(n2 // 16, 16, -1), g.reshape(n2 // 16, 16, -1)], 1).reshape(2 * n2, -1)
+    bh, bg = b1[:n2], b1[n2:]
+    b = torch.stack([bh.reshape(-1, 16), bg.reshape(-1, 16)], 1).reshape(-1)
+    return w, b

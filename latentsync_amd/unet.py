@@ -1,0 +1,567 @@
+"""UNet3DConditionModel -- MI355X-native drop-in for
+latentsync/models/unet.py:39-512.
+
+Same constructor kwargs (the configs/unet/*.yaml ``model:`` schema), same
+``from_pretrained(model_config, ckpt_path, device)`` / ``load_state_dict`` drop
+rules / ``forward(sample, timestep, encoder_hidden_states, ...)`` signature and
+``UNet3DConditionOutput(sample=...)`` result.  Underneath, every op runs in the
+HIP C-ABI library (latentsync_amd/ops.py -> libls_hip.so) on NHWC bf16
+activations with frames folded into the image index:
+
+  ResnetBlock3D (resnet.py:182-223)
+      GN5D stats -> conv1 3x3 [GN-apply+SiLU prologue, bias + temb epilogue]
+      GN5D stats -> conv2 3x3 [GN-apply+SiLU prologue, bias + shortcut residual]
+      the up-block torch.cat (unet_blocks.py:624,745) is fused into the gathers.
+  Transformer3DModel (attention.py:82-124) + BasicTransformerBlock (:174-199)
+      GN4D stats -> proj_in 1x1 [GN prologue] -> LN -> fused q|k|v GEMM ->
+      flash attention -> out-proj [bias + residual] -> LN -> q GEMM, audio k|v
+      GEMM -> attention (Nk = 50) -> out-proj -> LN -> GEGLU GEMM (fused
+      h * gelu(g) epilogue) -> FF2 [bias + residual] -> proj_out [+ residual]
+  VanillaTemporalModule (motion_module.py:39-313)
+      GN4D -> proj_in [GN prologue] -> 2 x (LN + pos-enc -> q|k|v -> temporal
+      attention over frames via strided views -> out-proj) -> GEGLU FF -> proj_out
+"""
+import math
+from dataclasses import dataclass
+
+import torch
+
+from . import ops
+from .config import STAGE2_MODEL
+from .packing import geglu_interleave, pack_weight, pad_bias
+from .schema import unet_param_shapes
+from .weights import fill_state_dict
+
+_DEFAULTS = dict(
+    sample_size=None, in_channels=4, out_channels=4, center_input_sample=False, flip_sin_to_cos=True, freq_shift=0,
+    down_block_types=("CrossAttnDownBlock3D", "CrossAttnDownBlock3D", "CrossAttnDownBlock3D", "DownBlock3D"),
+    mid_block_type="UNetMidBlock3DCrossAttn",
+    up_block_types=("UpBlock3D", "CrossAttnUpBlock3D", "CrossAttnUpBlock3D", "CrossAttnUpBlock3D"),
+    only_cross_attention=False, block_out_channels=(320, 640, 1280, 1280), layers_per_block=2, downsample_padding=1,
+    mid_block_scale_factor=1, act_fn="silu", norm_num_groups=32, norm_eps=1e-5, cross_attention_dim=1280,
+    attention_head_dim=8, dual_cross_attention=False, use_linear_projection=False, class_embed_type=None,
+    num_class_embeds=None, upcast_attention=False, resnet_time_scale_shift="default", use_inflated_groupnorm=False,
+    use_motion_module=False, motion_module_resolutions=(1, 2, 4, 8), motion_module_mid_block=False,
+    motion_module_decoder_only=False, motion_module_type=None, motion_module_kwargs={}, add_audio_layer=False,
+)
+
+
+class FrozenDict(dict):
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError as e:
+            raise AttributeError(k) from e
+
+
+@dataclass
+class UNet3DConditionOutput:
+    sample: torch.Tensor
+
+    def __getitem__(self, i):
+        return (self.sample,)[i]
+
+
+def positional_encoding(d_model, max_len=24):
+    """PositionalEncoding buffer (motion_module.py:221-230)."""
+    position = torch.arange(max_len).unsqueeze(1)
+    div_term = torch.exp(torch.arange(0, d_model, 2) * (-math.log(10000.0) / d_model))
+    pe = torch.zeros(max_len, d_model)
+    pe[:, 0::2] = torch.sin(position * div_term)
+    pe[:, 1::2] = torch.cos(position * div_term)
+    return pe
+
+
+# --------------------------------------------------------------------------
+# packed device-side layers
+# --------------------------------------------------------------------------
+
+
+class _Dev:
+    def __init__(self, sd, device):
+        self.sd, self.device = sd, device
+
+    def f32(self, key):
+        return self.sd[key].float().to(self.device).contiguous()
+
+    def packed(self, wkey, bkey=None, ksize=None, cin_pad=None, n_pad=None, w=None, b=None, geglu=False):
+        w = self.sd[wkey] if w is None else w
+        b = (self.sd.get(bkey) if bkey else None) if b is None else b
+        if ksize is None:
+            ksize = w.shape[-1] if w.dim() == 4 else 1
+        n_out = w.shape[0]
+        if geglu:
+            w, b = geglu_interleave(w.float(), b.float())
+        wp = pack_weight(w, cin_pad=cin_pad, n_pad=n_pad)
+        bp = pad_bias(b, n_pad)
+        cin = wp.shape[1] // (ksize * ksize) if ksize == 1 else None
+        if ksize == 3:
+            i = w.shape[1]
+            cin = cin_pad or (i + 7) // 8 * 8
+        elif ksize == 1:
+            i = w.shape[1]
+            cin = cin_pad or (i + 7) // 8 * 8
+        return ops.Packed(wp.to(torch.bfloat16).to(self.device).contiguous(),
+                          None if bp is None else bp.to(self.device).contiguous(), cin, ksize, n_out, geglu)
+
+
+class _Resnet:
+    def __init__(self, dv, p, cin, cout, groups, eps, out_scale, temb_slot):
+        self.groups, self.eps, self.cin, self.cout = groups, eps, cin, cout
+        self.n1 = (dv.f32(p + ".norm1.weight"), dv.f32(p + ".norm1.bias"))
+        self.n2 = (dv.f32(p + ".norm2.weight"), dv.f32(p + ".norm2.bias"))
+        self.c1 = dv.packed(p + ".conv1.weight", p + ".conv1.bias")
+        self.c2 = dv.packed(p + ".conv2.weight", p + ".conv2.bias")
+        self.sc = dv.packed(p + ".conv_shortcut.weight", p + ".conv_shortcut.bias") \
+            if (p + ".conv_shortcut.weight") in dv.sd else None
+        self.out_scale = 1.0 / out_scale
+        self.temb_slot = temb_slot  # column offset into the batched temb projection
+
+    def __call__(self, x, B, temb_all, x2=None):
+        n = x.shape[0]
+        F = n // B
+        pps = F * x.shape[1] * x.shape[2]
+        s1 = ops.group_norm(x, self.groups, self.eps, *self.n1, B, x2=x2)
+        h = ops.conv(x, self.c1, x2=x2, aff=(s1[0], s1[1], F, True),
+                     rowvec=(temb_all[:, self.temb_slot:], pps, temb_all.shape[1]))
+        s2 = ops.group_norm(h, self.groups, self.eps, *self.n2, B)
+        res = x if self.sc is None else ops.conv(x, self.sc, x2=x2)
+        return ops.conv(h, self.c2, aff=(s2[0], s2[1], F, True), res=res, out_scale=self.out_scale)
+
+
+class _Transformer:
+    def __init__(self, dv, p, c, heads, groups, audio):
+        self.c, self.heads, self.groups = c, heads, groups
+        self.norm = (dv.f32(p + ".norm.weight"), dv.f32(p + ".norm.bias"))
+        self.proj_in = dv.packed(p + ".proj_in.weight", p + ".proj_in.bias")
+        self.proj_out = dv.packed(p + ".proj_out.weight", p + ".proj_out.bias")
+        b = p + ".transformer_blocks.0"
+        sd = dv.sd
+        self.ln1 = (dv.f32(b + ".norm1.weight"), dv.f32(b + ".norm1.bias"))
+        self.qkv1 = dv.packed(None, w=torch.cat([sd[f"{b}.attn1.to_{n}.weight"] for n in "qkv"], 0))
+        self.o1 = dv.packed(b + ".attn1.to_out.0.weight", b + ".attn1.to_out.0.bias")
+        self.has_audio = audio and (b + ".attn2.to_q.weight") in sd
+        if self.has_audio:
+            self.ln2 = (dv.f32(b + ".norm2.weight"), dv.f32(b + ".norm2.bias"))
+            self.q2 = dv.packed(b + ".attn2.to_q.weight")
+            self.kv2 = dv.packed(None, w=torch.cat([sd[b + ".attn2.to_k.weight"], sd[b + ".attn2.to_v.weight"]], 0))
+            self.o2 = dv.packed(b + ".attn2.to_out.0.weight", b + ".attn2.to_out.0.bias")
+        self.ln3 = (dv.f32(b + ".norm3.weight"), dv.f32(b + ".norm3.bias"))
+        self.ff1 = dv.packed(b + ".ff.net.0.proj.weight", b + ".ff.net.0.proj.bias", geglu=True)
+        self.ff2 = dv.packed(b + ".ff.net.2.weight", b + ".ff.net.2.bias")
+
+    def __call__(self, x, audio_rows, n_audio_tok):
+        n, H, W, C = x.shape
+        HW = H * W
+        rows = n * HW
+        d = C // self.heads
+        sc = ops.group_norm(x, self.groups, 1e-6, *self.norm, n)
+        h = ops.conv(x, self.proj_in, aff=(sc[0], sc[1], 1, False)).view(rows, C)
+        # self attention
+        t = ops.layer_norm(h, *self.ln1)
+        qkv = ops.linear(t, self.qkv1)
+        o = torch.empty((rows, C), dtype=torch.bfloat16, device=x.device)
+        ops.attention(qkv, qkv[:, C:], qkv[:, 2 * C:], o, batch=n, z2=1, heads=self.heads, nq=HW, nk=HW, head_dim=d,
+                      qs=(HW * 3 * C, 0, 3 * C, d), ks=(HW * 3 * C, 0, 3 * C, d), vs=(HW * 3 * C, 0, 3 * C, d),
+                      os_=(HW * C, 0, C, d))
+        h = ops.linear(o, self.o1, res=h)
+        # audio cross attention
+        if self.has_audio and audio_rows is not None:
+            t = ops.layer_norm(h, *self.ln2)
+            q = ops.linear(t, self.q2)
+            kv = ops.linear(audio_rows, self.kv2)
+            L = n_audio_tok
+            ops.attention(q, kv, kv[:, C:], o, batch=n, z2=1, heads=self.heads, nq=HW, nk=L, head_dim=d,
+                          qs=(HW * C, 0, C, d), ks=(L * 2 * C, 0, 2 * C, d), vs=(L * 2 * C, 0, 2 * C, d),
+                          os_=(HW * C, 0, C, d))
+            h = ops.linear(o, self.o2, res=h)
+        # GEGLU feed-forward
+        t = ops.layer_norm(h, *self.ln3)
+        g = ops.linear(t, self.ff1, act=ops.ACT_GEGLU)
+        h = ops.linear(g, self.ff2, res=h)
+        return ops.conv(h.view(n, H, W, C), self.proj_out, res=x)
+
+
+class _Motion:
+    def __init__(self, dv, p, c, heads, groups, kw):
+        t = p + ".temporal_transformer"
+        b = t + ".transformer_blocks.0"
+        sd = dv.sd
+        self.c, self.heads, self.groups = c, heads, groups
+        self.norm = (dv.f32(t + ".norm.weight"), dv.f32(t + ".norm.bias"))
+        self.proj_in = dv.packed(t + ".proj_in.weight", t + ".proj_in.bias")
+        self.proj_out = dv.packed(t + ".proj_out.weight", t + ".proj_out.bias")
+        self.attn = []
+        i = 0
+        max_len = kw.get("temporal_position_encoding_max_len", 24)
+        while f"{b}.attention_blocks.{i}.to_q.weight" in sd:
+            a = f"{b}.attention_blocks.{i}"
+            pe = sd.get(a + ".pos_encoder.pe")
+            if kw.get("temporal_position_encoding", False):
+                pe = (pe.reshape(-1, c) if pe is not None else positional_encoding(c, max_len)).float()
+                pe = pe.to(dv.device).contiguous()
+            else:
+                pe = None
+            self.attn.append(dict(
+                ln=(dv.f32(f"{b}.norms.{i}.weight"), dv.f32(f"{b}.norms.{i}.bias")),
+                qkv=dv.packed(None, w=torch.cat([sd[f"{a}.to_{n}.weight"] for n in "qkv"], 0)),
+                o=dv.packed(a + ".to_out.0.weight", a + ".to_out.0.bias"), pe=pe))
+            i += 1
+        self.ffn = (dv.f32(b + ".ff_norm.weight"), dv.f32(b + ".ff_norm.bias"))
+        self.ff1 = dv.packed(b + ".ff.net.0.proj.weight", b + ".ff.net.0.proj.bias", geglu=True)
+        self.ff2 = dv.packed(b + ".ff.net.2.weight", b + ".ff.net.2.bias")
+
+    def __call__(self, x, B):
+        n, H, W, C = x.shape
+        F = n // B
+        S = H * W
+        rows = n * S
+        d = C // self.heads
+        sc = ops.group_norm(x, self.groups, 1e-6, *self.norm, n)
+        h = ops.conv(x, self.proj_in, aff=(sc[0], sc[1], 1, False)).view(rows, C)
+        o = torch.empty((rows, C), dtype=torch.bfloat16, device=x.device)
+        for a in self.attn:
+            t = ops.layer_norm(h, *a["ln"], pe=a["pe"], pe_rows_per_frame=S, pe_frames=F)
+            qkv = ops.linear(t, a["qkv"])
+            # "(b f) s c -> (b s) f c": batch (b, s), sequence f
+            st = (F * S * 3 * C, 3 * C, S * 3 * C, d)
+            ops.attention(qkv, qkv[:, C:], qkv[:, 2 * C:], o, batch=B * S, z2=S, heads=self.heads, nq=F, nk=F,
+                          head_dim=d, qs=st, ks=st, vs=st, os_=(F * S * C, C, S * C, d))
+            h = ops.linear(o, a["o"], res=h)
+        t = ops.layer_norm(h, *self.ffn)
+        g = ops.linear(t, self.ff1, act=ops.ACT_GEGLU)
+        h = ops.linear(g, self.ff2, res=h)
+        return ops.conv(h.view(n, H, W, C), self.proj_out, res=x)
+
+
+class _DeviceUNet:
+    """All packed weights on one device + the forward schedule."""
+
+    def __init__(self, sd, cfg, device):
+        dv = _Dev(sd, device)
+        self.cfg, self.device = cfg, device
+        boc = list(cfg["block_out_channels"])
+        nb = len(boc)
+        heads = cfg["attention_head_dim"]
+        heads = list(heads) if isinstance(heads, (list, tuple)) else [heads] * nb
+        groups, eps = cfg["norm_num_groups"], float(cfg["norm_eps"])
+        lpb = cfg["layers_per_block"]
+        audio = cfg["add_audio_layer"]
+        mkw = cfg.get("motion_module_kwargs") or {}
+        mheads = mkw.get("num_attention_heads", 8)
+        self.cin = cfg["in_channels"]
+        self.cin_pad = (self.cin + 7) // 8 * 8
+        self.cout = cfg["out_channels"]
+        self.boc = boc
+        self.temb_dim = boc[0] * 4
+        self.flip, self.shift = bool(cfg["flip_sin_to_cos"]), float(cfg["freq_shift"])
+        self.t1 = dv.packed("time_embedding.linear_1.weight")
+        self.t1b = dv.f32("time_embedding.linear_1.bias")
+        self.t2 = dv.packed("time_embedding.linear_2.weight")
+        self.t2b = dv.f32("time_embedding.linear_2.bias")
+        self.conv_in = dv.packed("conv_in.weight", "conv_in.bias", cin_pad=self.cin_pad)
+        temb_w, temb_b = [], []
+
+        def resnet(p, cin, cout, scale=1.0):
+            slot = sum(w.shape[0] for w in temb_w)
+            temb_w.append(sd[p + ".time_emb_proj.weight"])
+            temb_b.append(sd[p + ".time_emb_proj.bias"])
+            return _Resnet(dv, p, cin, cout, groups, eps, scale, slot)
+
+        def motion(p, c):
+            if f"{p}.temporal_transformer.norm.weight" not in sd:
+                return None
+            return _Motion(dv, p, c, mheads, groups, mkw)
+
+        self.down = []
+        out_c = boc[0]
+        for i, bt in enumerate(cfg["down_block_types"]):
+            in_c, out_c = out_c, boc[i]
+            layers = []
+            for l in range(lpb):
+                p = f"down_blocks.{i}"
+                r = resnet(f"{p}.resnets.{l}", in_c if l == 0 else out_c, out_c)
+                a = _Transformer(dv, f"{p}.attentions.{l}", out_c, heads[i], groups, audio) \
+                    if bt == "CrossAttnDownBlock3D" else None
+                layers.append((r, a, motion(f"{p}.motion_modules.{l}", out_c)))
+            ds = dv.packed(f"down_blocks.{i}.downsamplers.0.conv.weight", f"down_blocks.{i}.downsamplers.0.conv.bias") \
+                if i < nb - 1 else None
+            self.down.append((layers, ds))
+        c = boc[-1]
+        ms = float(cfg["mid_block_scale_factor"])
+        self.mid = (resnet("mid_block.resnets.0", c, c, ms),
+                    _Transformer(dv, "mid_block.attentions.0", c, heads[-1], groups, audio),
+                    motion("mid_block.motion_modules.0", c),
+                    resnet("mid_block.resnets.1", c, c, ms))
+        rev = list(reversed(boc))
+        rheads = list(reversed(heads))
+        self.up = []
+        out_c = rev[0]
+        for i, bt in enumerate(cfg["up_block_types"]):
+            prev_c, out_c = out_c, rev[i]
+            in_c = rev[min(i + 1, nb - 1)]
+            layers = []
+            for l in range(lpb + 1):
+                p = f"up_blocks.{i}"
+                skip_c = in_c if l == lpb else out_c
+                r_in = prev_c if l == 0 else out_c
+                r = resnet(f"{p}.resnets.{l}", r_in + skip_c, out_c)
+                a = _Transformer(dv, f"{p}.attentions.{l}", out_c, rheads[i], groups, audio) \
+                    if bt == "CrossAttnUpBlock3D" else None
+                layers.append((r, a, motion(f"{p}.motion_modules.{l}", out_c)))
+            us = dv.packed(f"up_blocks.{i}.upsamplers.0.conv.weight", f"up_blocks.{i}.upsamplers.0.conv.bias") \
+                if i < nb - 1 else None
+            self.up.append((layers, us))
+        self.norm_out = (dv.f32("conv_norm_out.weight"), dv.f32("conv_norm_out.bias"))
+        self.groups, self.eps = groups, eps
+        self.conv_out = dv.packed("conv_out.weight", "conv_out.bias")
+        self.temb_w = torch.cat(temb_w, 0).to(torch.bfloat16).to(device).contiguous()
+        self.temb_b = torch.cat(temb_b, 0).float().to(device).contiguous()
+
+    def temb(self, ts_i32, step_i32, B):
+        t = ops.timestep_embed(ts_i32, step_i32, B, self.boc[0], self.flip, self.shift)
+        e1 = ops.small_linear(t, self.t1.w, self.t1b)
+        emb = ops.small_linear(e1, self.t2.w, self.t2b, silu_in=True)
+        return ops.small_linear(emb, self.temb_w, self.temb_b, silu_in=True)
+
+    def forward(self, x_in, B, ts_i32, step_i32, audio_rows, n_audio_tok, down_res=None, mid_res=None):
+        """x_in NHWC bf16 (B*F, H, W, cin_pad) -> eps NHWC bf16 (B*F, H, W, out_channels)."""
+        temb = self.temb(ts_i32, step_i32, B)
+        h = ops.conv(x_in, self.conv_in)
+        skips = [h]
+        for layers, ds in self.down:
+            for r, a, m in layers:
+                h = r(h, B, temb)
+                if a is not None:
+                    h = a(h, audio_rows, n_audio_tok)
+                if m is not None:
+                    h = m(h, B)
+                skips.append(h)
+            if ds is not None:
+                h = ops.conv(h, ds, stride=2, pad=1)
+                skips.append(h)
+        if down_res is not None:
+            skips = [s + r for s, r in zip(skips, down_res)]
+        r0, a, m, r1 = self.mid
+        h = r0(h, B, temb)
+        h = a(h, audio_rows, n_audio_tok)
+        if m is not None:
+            h = m(h, B)
+        h = r1(h, B, temb)
+        if mid_res is not None:
+            h = h + mid_res
+        for layers, us in self.up:
+            for r, a, m in layers:
+                h = r(h, B, temb, x2=skips.pop())
+                if a is not None:
+                    h = a(h, audio_rows, n_audio_tok)
+                if m is not None:
+                    h = m(h, B)
+            if us is not None:
+                h = ops.conv(h, us, upsample=True)
+        sc = ops.group_norm(h, self.groups, self.eps, *self.norm_out, B)
+        F = h.shape[0] // B
+        return ops.conv(h, self.conv_out, aff=(sc[0], sc[1], F, True))
+
+
+# --------------------------------------------------------------------------
+# public drop-in class
+# --------------------------------------------------------------------------
+
+
+class UNet3DConditionModel(torch.nn.Module):
+    """Drop-in for latentsync.models.unet.UNet3DConditionModel (unet.py:39-512)."""
+
+    _supports_gradient_checkpointing = False
+
+    def __init__(self, **kwargs):
+        super().__init__()
+        unknown = set(kwargs) - set(_DEFAULTS)
+        if unknown:
+            raise TypeError(f"unexpected UNet3DConditionModel arguments: {sorted(unknown)}")
+        cfg = dict(_DEFAULTS)
+        cfg.update(kwargs)
+        cfg["norm_eps"] = float(cfg["norm_eps"])
+        if cfg["mid_block_type"] != "UNetMidBlock3DCrossAttn":
+            raise ValueError(f"unknown mid_block_type : {cfg['mid_block_type']}")
+        for bt in list(cfg["down_block_types"]) + list(cfg["up_block_types"]):
+            bt = bt[7:] if bt.startswith("UNetRes") else bt
+            if bt not in ("DownBlock3D", "CrossAttnDownBlock3D", "UpBlock3D", "CrossAttnUpBlock3D"):
+                raise ValueError(f"{bt} does not exist.")
+        if cfg["dual_cross_attention"]:
+            raise NotImplementedError
+        if cfg["use_linear_projection"] or cfg["class_embed_type"] or cfg["num_class_embeds"] or \
+                cfg["resnet_time_scale_shift"] != "default" or cfg["use_inflated_groupnorm"]:
+            raise NotImplementedError("configuration outside the LatentSync inference path")
+        self._internal_dict = FrozenDict(cfg)
+        self.sample_size = cfg["sample_size"]
+        self.use_motion_module = cfg["use_motion_module"]
+        self.add_audio_layer = cfg["add_audio_layer"]
+        self._shapes = unet_param_shapes(cfg)
+        # reference __init__ draws nn defaults; weights here come from the
+        # deterministic generator until a checkpoint is loaded.
+        self._sd = fill_state_dict(self._shapes, 0)
+        for k in self._shapes:
+            if k.endswith("pos_encoder.pe"):
+                self._sd[k] = positional_encoding(self._shapes[k][-1], self._shapes[k][1])[None]
+        self._device = torch.device("cpu")
+        self._dev = None
+        self.num_upsamplers = len(cfg["block_out_channels"]) - 1
+
+    # -- config / attributes the pipeline reads ----------------------------
+    @property
+    def config(self):
+        return self._internal_dict
+
+    @property
+    def dtype(self):
+        return torch.bfloat16
+
+    @property
+    def device(self):
+        return self._device
+
+    @classmethod
+    def from_config(cls, config):
+        return cls(**dict(config))
+
+    def set_attention_slice(self, slice_size):
+        """Accepted for API compatibility (unet.py:243-306); the flash kernel never
+        materialises the attention matrix, so slicing is a no-op."""
+        return None
+
+    # -- weights ------------------------------------------------------------
+    def state_dict(self, *a, **k):
+        return dict(self._sd)
+
+    def load_state_dict(self, state_dict, strict=True):
+        """unet.py:473-492 drop rules, then strict/non-strict key matching."""
+        state_dict = dict(state_dict)
+        if "conv_in.weight" in state_dict and state_dict["conv_in.weight"].shape[1] != self.config.in_channels:
+            del state_dict["conv_in.weight"]
+            state_dict.pop("conv_in.bias", None)
+        if "conv_out.weight" in state_dict and state_dict["conv_out.weight"].shape[0] != self.config.out_channels:
+            del state_dict["conv_out.weight"]
+            state_dict.pop("conv_out.bias", None)
+        for key in [k for k in state_dict if "attn2.to_k." in k or "attn2.to_v." in k]:
+            if state_dict[key].shape[1] != self.config.cross_attention_dim:
+                del state_dict[key]
+        missing = [k for k in self._shapes if k not in state_dict]
+        unexpected = [k for k in state_dict if k not in self._shapes]
+        if strict and (missing or unexpected):
+            raise RuntimeError(f"Error(s) in loading state_dict: missing {missing[:5]}, unexpected {unexpected[:5]}")
+        for k, v in state_dict.items():
+            if k in self._shapes:
+                if tuple(v.shape) != tuple(self._shapes[k]):
+                    raise RuntimeError(f"size mismatch for {k}: {tuple(v.shape)} vs {self._shapes[k]}")
+                self._sd[k] = v.detach().float().cpu()
+        self._dev = None
+        if self._device.type == "cuda":
+            self._pack()
+        return missing, unexpected
+
+    @classmethod
+    def from_pretrained(cls, model_config: dict, ckpt_path: str, device="cpu"):
+        """unet.py:494-512: (unet, resume_global_step)."""
+        unet = cls.from_config(model_config)
+        step = 0
+        if ckpt_path != "":
+            ckpt = torch.load(ckpt_path, map_location="cpu", weights_only=True)
+            step = ckpt.get("global_step", 0)
+            unet.load_state_dict(ckpt["state_dict"], strict=False)
+        return unet.to(device), step
+
+    def init_weights(self, seed: int):
+        """Deterministic reference-independent weights (latentsync_amd.weights)."""
+        sd = fill_state_dict(self._shapes, seed)
+        for k, v in sd.items():
+            self._sd[k] = v
+        self._dev = None
+        if self._device.type == "cuda":
+            self._pack()
+        return self
+
+    def _pack(self):
+        self._dev = _DeviceUNet(self._sd, self.config, self._device)
+
+    def to(self, device=None, dtype=None, *a, **k):
+        if isinstance(device, torch.dtype):
+            device, dtype = None, device
+        if device is not None:
+            device = torch.device(device)
+            if device.type == "cuda" and device.index is None:
+                device = torch.device("cuda", torch.cuda.current_device())
+            if device != self._device:
+                self._device = device
+                self._dev = None
+                if device.type == "cuda":
+                    self._pack()
+        return self
+
+    def cuda(self, device=None):
+        return self.to(torch.device("cuda", device) if device is not None else "cuda")
+
+    def train(self, mode=True):
+        if mode:
+            raise NotImplementedError("training is out of scope (SURVEY.md §2)")
+        self.training = False
+        return self
+
+    def eval(self):
+        self.training = False
+        return self
+
+    # -- forward -------------------------------------------------------------
+    def _require_device(self):
+        if self._dev is None:
+            raise RuntimeError("UNet3DConditionModel runs only on the MI355X HIP path: call .to('cuda') first")
+        return self._dev
+
+    def forward(self, sample, timestep, encoder_hidden_states=None, class_labels=None, attention_mask=None,
+                down_block_additional_residuals=None, mid_block_additional_residual=None, return_dict=True):
+        """unet.py:312-471.  ``attention_mask`` is accepted and, as in the reference
+        (whose down/up blocks never forward it to the attention), has no effect."""
+        dev = self._require_device()
+        B, Cin, F, H, W = sample.shape
+        if Cin != self.config.in_channels:
+            raise ValueError(f"expected {self.config.in_channels} input channels, got {Cin}")
+        if H % (2 ** self.num_upsamplers) or W % (2 ** self.num_upsamplers):
+            raise NotImplementedError("sample size must be a multiple of the overall up-sampling factor")
+        if self.config.center_input_sample:
+            sample = 2 * sample - 1.0
+        x = torch.zeros((B * F, H, W, dev.cin_pad), dtype=torch.bfloat16, device=sample.device)
+        x[..., :Cin] = sample.permute(0, 2, 3, 4, 1).reshape(B * F, H, W, Cin)
+        t = int(timestep.reshape(-1)[0].item()) if torch.is_tensor(timestep) else int(timestep)
+        ts = torch.tensor([t], dtype=torch.int32, device=sample.device)
+        step = torch.zeros(1, dtype=torch.int32, device=sample.device)
+        audio, ntok = None, 0
+        if encoder_hidden_states is not None and self.add_audio_layer:
+            ehs = encoder_hidden_states
+            if ehs.dim() == 4:
+                ehs = ehs.reshape(-1, ehs.shape[-2], ehs.shape[-1])
+            ntok = ehs.shape[1]
+            audio = ehs.to(torch.bfloat16).reshape(-1, ehs.shape[-1]).contiguous()
+        dres = None
+        if down_block_additional_residuals is not None:
+            dres = []
+            for r in down_block_additional_residuals:
+                if r.dim() == 4:
+                    r = r.unsqueeze(2)
+                rb, rc, rf, rh, rw = r.shape
+                dres.append(r.expand(B, rc, F, rh, rw).permute(0, 2, 3, 4, 1).reshape(B * F, rh, rw, rc)
+                            .to(torch.bfloat16))
+        mres = None
+        if mid_block_additional_residual is not None:
+            r = mid_block_additional_residual
+            if r.dim() == 4:
+                r = r.unsqueeze(2)
+            rb, rc, rf, rh, rw = r.shape
+            mres = r.expand(B, rc, F, rh, rw).permute(0, 2, 3, 4, 1).reshape(B * F, rh, rw, rc).to(torch.bfloat16)
+        eps = dev.forward(x, B, ts, step, audio, ntok, dres, mres)
+        out = eps.reshape(B, F, H, W, -1)[..., :self.config.out_channels].permute(0, 4, 1, 2, 3)
+        out = out.to(sample.dtype if sample.dtype.is_floating_point else torch.float32).contiguous()
+        if not return_dict:
+            return (out,)
+        return UNet3DConditionOutput(sample=out)
+
+    __call__ = torch.nn.Module.__call__

@@ -1,0 +1,225 @@
+"""Per-kernel parity on MI355X: every C-ABI entry point against a plain
+PyTorch fp32 CPU reference of the same op, on the same bf16-rounded inputs.
+Tolerances are stated per test (bf16 output rounding + fp32 accumulation)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import rel_err
+from latentsync_amd import ops
+from latentsync_amd.packing import geglu_interleave, pack_weight, pad_bias
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+def rnd(*shape, seed=0, scale=1.0):
+    return torch.randn(*shape, generator=torch.Generator().manual_seed(seed)) * scale
+
+
+def packed(w, b, ksize, cin_pad=None, geglu=False, n_pad=None):
+    n_out = w.shape[0]
+    if geglu:
+        w, b = geglu_interleave(w, b)
+    wp = pack_weight(w, cin_pad=cin_pad, n_pad=n_pad)
+    bp = pad_bias(b, n_pad)
+    cin = cin_pad or (w.shape[1] + 7) // 8 * 8
+    return ops.Packed(wp.to(torch.bfloat16).to(DEV), None if bp is None else bp.to(DEV), cin, ksize, n_out, geglu)
+
+
+def nhwc(x):  # (n, C, H, W) -> (n, H, W, C) bf16 device
+    return x.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(DEV)
+
+
+def nchw(y):
+    return y.float().cpu().permute(0, 3, 1, 2)
+
+
+@pytest.mark.parametrize("cin,cout,stride,up,split", [(64, 96, 1, False, 0), (64, 64, 2, False, 0),
+                                                      (16, 320, 1, False, 0), (128, 64, 1, True, 0),
+                                                      (640, 1280, 1, False, 4), (8, 40, 1, False, 0)])
+def test_conv3x3(gpu, cin, cout, stride, up, split):
+    n, H = 3, 8
+    x = bf(rnd(n, cin, H, H, seed=1))
+    w = bf(rnd(cout, cin, 3, 3, seed=2, scale=1 / math.sqrt(9 * cin)))
+    b = rnd(cout, seed=3, scale=0.1)
+    xin = F.interpolate(x, scale_factor=2.0, mode="nearest") if up else x
+    ref = F.conv2d(xin, w, b, stride=stride, padding=1)
+    y = ops.conv(nhwc(x), packed(w, b, 3), stride=stride, upsample=up, split_k=split)
+    assert rel_err(nchw(y), ref) < 1e-2
+
+
+def test_conv3x3_vae_downsample(gpu):
+    x = bf(rnd(2, 64, 8, 8, seed=4))
+    w = bf(rnd(64, 64, 3, 3, seed=5, scale=1 / 24))
+    b = rnd(64, seed=6, scale=0.1)
+    ref = F.conv2d(F.pad(x, (0, 1, 0, 1)), w, b, stride=2)
+    y = ops.conv(nhwc(x), packed(w, b, 3), stride=2, pad=0, out_hw=(4, 4))
+    assert rel_err(nchw(y), ref) < 1e-2
+
+
+def test_conv_groupnorm_silu_temb_residual_concat(gpu):
+    """ResnetBlock3D conv1/conv2 fusion: GN5D(+SiLU) prologue, temb + residual
+    epilogue, concat (x, skip) gather."""
+    B, Fr, H, c1, c2, cout, groups = 2, 4, 8, 64, 32, 64, 32
+    x1 = bf(rnd(B * Fr, c1, H, H, seed=7))
+    x2 = bf(rnd(B * Fr, c2, H, H, seed=8))
+    xc = torch.cat([x1, x2], 1)
+    gamma, beta = 1 + 0.1 * rnd(c1 + c2, seed=9), 0.1 * rnd(c1 + c2, seed=10)
+    w = bf(rnd(cout, c1 + c2, 3, 3, seed=11, scale=1 / math.sqrt(9 * (c1 + c2))))
+    b = rnd(cout, seed=12, scale=0.1)
+    temb = rnd(B, cout, seed=13)
+    res = bf(rnd(B * Fr, cout, H, H, seed=14))
+    x5 = xc.reshape(B, Fr, c1 + c2, H, H).permute(0, 2, 1, 3, 4)
+    g5 = F.silu(F.group_norm(x5, groups, gamma, beta, 1e-5))
+    g4 = g5.permute(0, 2, 1, 3, 4).reshape(B * Fr, c1 + c2, H, H)
+    ref = F.conv2d(g4, w, b, padding=1) + temb.repeat_interleave(Fr, 0)[:, :, None, None]
+    ref = (ref + res) * 0.5
+    sc, sh = ops.group_norm(nhwc(x1), groups, 1e-5, gamma.to(DEV), beta.to(DEV), B, x2=nhwc(x2))
+    y = ops.conv(nhwc(x1), packed(w, b, 3), x2=nhwc(x2), aff=(sc, sh, Fr, True),
+                 rowvec=(temb.to(DEV), Fr * H * H, cout), res=nhwc(res), out_scale=0.5)
+    assert rel_err(nchw(y), ref) < 1e-2
+
+
+@pytest.mark.parametrize("C,groups,spp", [(320, 32, 16), (2560, 32, 1), (128, 32, 1), (96, 32, 4)])
+def test_groupnorm_stats(gpu, C, groups, spp):
+    n, H = 16, 4
+    x = bf(rnd(n, C, H, H, seed=20) * 3 + 5)  # large mean: exercises the shifted sums
+    gamma, beta = 1 + 0.1 * rnd(C, seed=21), 0.1 * rnd(C, seed=22)
+    S = n // spp
+    sc, sh = ops.group_norm(nhwc(x), groups, 1e-6, gamma.to(DEV), beta.to(DEV), S)
+    y = ops.affine_act(nhwc(x), sc, sh, S, False)
+    x5 = x.reshape(S, spp, C, H, H).permute(0, 2, 1, 3, 4)
+    ref = F.group_norm(x5, groups, gamma, beta, 1e-6).permute(0, 2, 1, 3, 4).reshape(n, C, H, H)
+    assert rel_err(nchw(y), ref) < 1e-2
+
+
+@pytest.mark.parametrize("M,K,N,act,split", [(200, 320, 960, 0, 0), (256, 1280, 10240, 1, 0),
+                                              (100, 384, 640, 0, 0), (256, 5120, 1280, 0, 3),
+                                              (64, 640, 5120, 1, 2), (300, 384, 1536, 2, 0)])
+def test_linear(gpu, M, K, N, act, split):
+    x = bf(rnd(M, K, seed=30))
+    w = bf(rnd(N, K, seed=31, scale=1 / math.sqrt(K)))
+    b = rnd(N, seed=32, scale=0.1)
+    res = bf(rnd(M, N // 2 if act == 1 else N, seed=33))
+    y_ref = x @ w.T + b
+    if act == ops.ACT_GEGLU:
+        h, g = y_ref.chunk(2, -1)
+        ref = h * F.gelu(g)
+        y = ops.linear(x.to(torch.bfloat16).to(DEV), packed(w, b, 1, geglu=True), act=act, split_k=split)
+    elif act == ops.ACT_GELU:
+        ref = F.gelu(y_ref)
+        y = ops.linear(x.to(torch.bfloat16).to(DEV), packed(w, b, 1), act=act, split_k=split)
+    else:
+        ref = y_ref + res
+        y = ops.linear(x.to(torch.bfloat16).to(DEV), packed(w, b, 1), res=res.to(torch.bfloat16).to(DEV),
+                       split_k=split)
+    assert rel_err(y.float().cpu(), ref) < 1e-2
+
+
+def test_linear_fp32_out(gpu):
+    x = bf(rnd(64, 512, seed=34))
+    w = bf(rnd(8, 512, seed=35, scale=1 / 16))
+    y = ops.linear(x.to(torch.bfloat16).to(DEV), packed(w, None, 1), out_f32=True)
+    assert y.dtype == torch.float32
+    assert rel_err(y.cpu(), x @ w.T) < 1e-5
+
+
+@pytest.mark.parametrize("C", [320, 1280, 384])
+def test_layernorm_pe(gpu, C):
+    rows, S, Fr = 4 * 16 * 2, 4, 16
+    x = bf(rnd(rows, C, seed=40) * 2 + 1)
+    g, b = 1 + 0.1 * rnd(C, seed=41), 0.1 * rnd(C, seed=42)
+    pe = rnd(24, C, seed=43)
+    ref = F.layer_norm(x, (C,), g, b, 1e-5)
+    f = (torch.arange(rows) // S) % Fr
+    ref = ref + pe[f]
+    y = ops.layer_norm(x.to(torch.bfloat16).to(DEV), g.to(DEV), b.to(DEV), 1e-5, pe=pe.to(DEV),
+                       pe_rows_per_frame=S, pe_frames=Fr)
+    assert rel_err(y.float().cpu(), ref) < 1e-2
+
+
+def _sdpa(q, k, v, scale=None):
+    return F.scaled_dot_product_attention(q, k, v, scale=scale)
+
+
+@pytest.mark.parametrize("n,N,Nk,heads,d", [(4, 256, 256, 8, 40), (2, 64, 64, 8, 80), (2, 16, 16, 8, 160),
+                                            (3, 256, 50, 8, 40), (2, 64, 50, 8, 160), (1, 100, 100, 6, 64),
+                                            (2, 64, 64, 1, 512), (2, 1024, 1024, 1, 128)])
+def test_attention_spatial(gpu, n, N, Nk, heads, d):
+    C = heads * d
+    q = bf(rnd(n, N, C, seed=50))
+    k = bf(rnd(n, Nk, C, seed=51))
+    v = bf(rnd(n, Nk, C, seed=52))
+    split = lambda t: t.reshape(t.shape[0], t.shape[1], heads, d).permute(0, 2, 1, 3)
+    ref = _sdpa(split(q), split(k), split(v)).permute(0, 2, 1, 3).reshape(n, N, C)
+    qd, kd, vd = (t.to(torch.bfloat16).to(DEV) for t in (q, k, v))
+    o = torch.empty_like(qd)
+    ops.attention(qd, kd, vd, o, batch=n, z2=1, heads=heads, nq=N, nk=Nk, head_dim=d, qs=(N * C, 0, C, d),
+                  ks=(Nk * C, 0, C, d), vs=(Nk * C, 0, C, d), os_=(N * C, 0, C, d))
+    assert rel_err(o.float().cpu(), ref) < 1.5e-2
+
+
+@pytest.mark.parametrize("C", [320, 1280])
+def test_attention_temporal_strided(gpu, C):
+    """VersatileAttention: '(b f) s c -> (b s) f c' read straight from the fused
+    q|k|v rows (motion_module.py:265, 300)."""
+    B, Fr, S, heads = 2, 16, 16, 8
+    d = C // heads
+    qkv = bf(rnd(B * Fr * S, 3 * C, seed=60))
+    q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
+    re = lambda t: t.reshape(B, Fr, S, C).permute(0, 2, 1, 3).reshape(B * S, Fr, heads, d).permute(0, 2, 1, 3)
+    o_ref = _sdpa(re(q), re(k), re(v)).permute(0, 2, 1, 3).reshape(B, S, Fr, C).permute(0, 2, 1, 3).reshape(-1, C)
+    qd = qkv.to(torch.bfloat16).to(DEV)
+    o = torch.empty((B * Fr * S, C), dtype=torch.bfloat16, device=DEV)
+    st = (Fr * S * 3 * C, 3 * C, S * 3 * C, d)
+    ops.attention(qd, qd[:, C:], qd[:, 2 * C:], o, batch=B * S, z2=S, heads=heads, nq=Fr, nk=Fr, head_dim=d, qs=st,
+                  ks=st, vs=st, os_=(Fr * S * C, C, S * C, d))
+    assert rel_err(o.float().cpu(), o_ref) < 1.5e-2
+
+
+def test_small_linear_and_timestep(gpu):
+    from oracle import ref_cpu as R
+    x = rnd(2, 1280, seed=70)
+    w = bf(rnd(3000, 1280, seed=71, scale=1 / 36))
+    b = rnd(3000, seed=72)
+    y = ops.small_linear(x.to(DEV), w.to(torch.bfloat16).to(DEV), b.to(DEV), silu_in=True)
+    assert rel_err(y.cpu(), F.silu(x) @ w.T + b) < 1e-5
+    ts = torch.tensor([951, 501, 1], dtype=torch.int32, device=DEV)
+    for i, t in enumerate((951, 501, 1)):
+        step = torch.tensor([i], dtype=torch.int32, device=DEV)
+        e = ops.timestep_embed(ts, step, 2, 320, True, 0.0)
+        ref = R.timestep_embedding(torch.tensor([t, t]), 320, True, 0)
+        assert (e.cpu() - ref).abs().max() < 2e-3  # sin/cos of args up to ~951 rad in fp32
+
+
+def test_ddim_cfg_step(gpu):
+    from oracle import ref_cpu as R
+    P, g = 4 * 8 * 8, 1.5
+    ac = R.ddim_alphas_cumprod()
+    ts = R.ddim_timesteps(20)
+    coef = []
+    for t in ts:
+        prev = t - 1000 // 20
+        a_t = ac[t]
+        a_p = ac[prev] if prev >= 0 else ac[0]
+        coef.append([a_t.sqrt(), (1 - a_t).sqrt(), a_p.sqrt(), (1 - a_p).sqrt()])
+    coef = torch.tensor(coef, dtype=torch.float32).to(DEV)
+    lat = rnd(P, 4, seed=80)
+    eps = bf(rnd(2 * P, 4, seed=81))
+    step = torch.tensor([3], dtype=torch.int32, device=DEV)
+    unet_in = torch.zeros((2 * P, 16), dtype=torch.bfloat16, device=DEV)
+    latd = lat.clone().to(DEV)
+    ops.ddim_cfg_step(eps.to(torch.bfloat16).to(DEV), 2, g, latd, coef, step, unet_in)
+    u, a = eps[:P], eps[P:]
+    ref = R.ddim_step(ac, u + g * (a - u), int(ts[3]), lat, 20)
+    assert rel_err(latd.cpu(), ref) < 1e-5
+    assert int(step.item()) == 4
+    assert rel_err(unet_in[:P, :4].float().cpu(), ref) < 1e-2
+    assert rel_err(unet_in[P:, :4].float().cpu(), ref) < 1e-2
