@@ -26,6 +26,15 @@ struct AttnArgs {
   float scale_log2;
 };
 
+// up to 8 bf16 from a possibly unaligned address, zero beyond `n`
+__device__ __forceinline__ uint4 load_partial(const u16* p, int n) {
+  u16 e[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) e[j] = j < n ? p[j] : (u16)0;
+  return make_uint4(e[0] | (uint32_t)e[1] << 16, e[2] | (uint32_t)e[3] << 16, e[4] | (uint32_t)e[5] << 16,
+                    e[6] | (uint32_t)e[7] << 16);
+}
+
 template <int DP, int NKF>
 __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
   constexpr int KC = DP / 32;   // 32-wide d chunks (QK^T k-steps)
@@ -53,7 +62,11 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
   for (int kc = 0; kc < KC; ++kc) {
     const int d = kc * 32 + lg * 8;
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (q0 + lq < a.nq && d < a.D) v = *(const uint4*)(qb + (long)(q0 + lq) * a.q_si + d);
+    if (q0 + lq < a.nq && d < a.D) {
+      const u16* src = qb + (long)(q0 + lq) * a.q_si + d;
+      if ((a.D & 7) == 0) v = *(const uint4*)src;
+      else v = load_partial(src, a.D - d);
+    }
     qf[kc] = __builtin_bit_cast(bf16x8, v);
   }
 
@@ -69,8 +82,13 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
       const int r = i / cpr, c = (i - r * cpr) * 8;
       uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
       if (t0 + r < a.nk && c < a.D) {
-        kv = *(const uint4*)(kb + (long)(t0 + r) * a.k_si + c);
-        vv = *(const uint4*)(vb + (long)(t0 + r) * a.v_si + c);
+        if ((a.D & 7) == 0) {
+          kv = *(const uint4*)(kb + (long)(t0 + r) * a.k_si + c);
+          vv = *(const uint4*)(vb + (long)(t0 + r) * a.v_si + c);
+        } else {  // head_dim not a multiple of 8 (reduced-width test configs)
+          kv = load_partial(kb + (long)(t0 + r) * a.k_si + c, a.D - c);
+          vv = load_partial(vb + (long)(t0 + r) * a.v_si + c, a.D - c);
+        }
       }
       *(uint4*)(Ks + r * PITCH + c) = kv;
       *(uint4*)(Vs + r * PITCH + c) = vv;
@@ -178,9 +196,9 @@ using namespace ls;
 
 extern "C" int ls_attention(const ls_attn_desc* d, void* stream) {
   if (!d || !d->q || !d->k || !d->v || !d->o) return fail(LS_ERR_INVALID, "ls_attention: null pointer");
-  if (d->head_dim % 8 || d->head_dim <= 0 || d->head_dim > 512 || d->nq <= 0 || d->nk <= 0 || d->batch <= 0 ||
+  if (d->head_dim % 2 || d->head_dim <= 0 || d->head_dim > 512 || d->nq <= 0 || d->nk <= 0 || d->batch <= 0 ||
       d->z2 <= 0 || d->heads <= 0)
-    return fail(LS_ERR_INVALID, "ls_attention: bad shape (head_dim % 8 == 0, <= 512)");
+    return fail(LS_ERR_INVALID, "ls_attention: bad shape (head_dim even, <= 512)");
   AttnArgs a;
   a.q = d->q; a.k = d->k; a.v = d->v; a.o = d->o;
   a.q_sb1 = d->q_sb1; a.q_sb2 = d->q_sb2; a.q_si = d->q_si; a.q_sh = d->q_sh;

@@ -179,11 +179,13 @@ def ddim_cfg_step(eps, Bu, guidance, lat, coef, step, unet_in):
                                _p(unet_in), unet_in.shape[-1], _stream()), "ls_ddim_cfg_step")
 
 
-def prep_pixels(faces_u8, mask, ld=8):
+def prep_pixels(faces_u8, mask, ld=8, pix=None, masked=None):
     lib = _lib.load()
     F_, _, R, _ = faces_u8.shape
-    pix = torch.empty((F_, R, R, ld), dtype=torch.bfloat16, device=faces_u8.device)
-    masked = torch.empty_like(pix)
+    if pix is None:
+        pix = torch.empty((F_, R, R, ld), dtype=torch.bfloat16, device=faces_u8.device)
+    if masked is None:
+        masked = torch.empty_like(pix)
     check(lib.ls_prep_pixels(_p(faces_u8), F_, R, _p(mask), _p(pix), _p(masked), ld, _stream()), "ls_prep_pixels")
     return pix, masked
 

@@ -1,0 +1,303 @@
+"""LipsyncPipeline -- drop-in for latentsync/pipelines/lipsync_pipeline.py:46-604
+on the MI355X HIP path.
+
+The per-window hot loop (lipsync_pipeline.py:500-575) runs in ``WindowEngine``:
+every tensor of a window is device-resident in static buffers, and the window is
+three captured hipGraphs replayed back to back --
+
+  encode : pixel prep (ImageProcessor.preprocess_fixed_mask_image) -> VAE encode
+           of masked + reference faces -> posterior sample * 0.18215 -> pack the
+           13-channel UNet input (prepare_mask_latents / prepare_image_latents,
+           :284-320, :547-549), reset the device step counter
+  step   : UNet3DConditionModel forward + CFG combine + DDIMScheduler.step +
+           re-pack of the next input (:540-562); the timestep and DDIM
+           coefficients are read on device at the step counter, so the SAME graph
+           replays num_inference_steps times
+  decode : latents / 0.18215 -> VAE decode -> paste_surrounding_pixels_back
+           (+ uint8 images for the all-gather / writer) (:145-149, :327-341, :571-574)
+
+Random draws are injected (initial latent noise, VAE posterior noise), as the
+parity harness requires (SURVEY.md §7 "RNG").
+"""
+import math
+import os
+
+import numpy as np
+import torch
+
+from . import ops
+
+SCALING = 0.18215
+
+
+def load_fixed_mask(resolution=256, mask_image_path=None):
+    """load_fixed_mask (image_processor.py:31-36) -> keep-mask (R, R) float32,
+    1 = keep the original pixel, 0 = mouth region to regenerate."""
+    if mask_image_path is None or not os.path.exists(mask_image_path):
+        bits = np.load(os.path.join(os.path.dirname(__file__), "assets", "fix_mask_256.npz"))["bits"]
+        m = np.unpackbits(bits)[: 256 * 256].reshape(256, 256).astype(np.float32)
+    else:
+        from PIL import Image
+        img = np.array(Image.open(mask_image_path).convert("RGB"))
+        m = (img[..., 0].astype(np.float64) / 255.0).astype(np.float32)
+    t = torch.from_numpy(m)
+    if t.shape[0] != resolution:
+        if resolution % t.shape[0] and t.shape[0] % resolution:
+            raise NotImplementedError("mask resize needs cv2 LANCZOS (out of scope); use a mask at the resolution")
+        t = torch.nn.functional.interpolate(t[None, None], size=(resolution, resolution), mode="nearest")[0, 0]
+    return t
+
+
+class WindowEngine:
+    """Device-resident executor of one 16-frame window; see module docstring."""
+
+    def __init__(self, unet, vae, scheduler, num_frames=16, resolution=256, num_inference_steps=20,
+                 guidance_scale=1.0, use_graphs=True, audio_tokens=50):
+        self.unet, self.vae, self.scheduler = unet, vae, scheduler
+        self.ud = unet._require_device()
+        self.vd = vae._require()
+        dev = unet.device
+        self.device = dev
+        self.F, self.R, self.h = num_frames, resolution, resolution // 8
+        self.steps, self.g = num_inference_steps, float(guidance_scale)
+        self.Bu = 2 if guidance_scale > 1.0 else 1
+        self.L = audio_tokens
+        self.P = self.F * self.h * self.h
+        scheduler.set_timesteps(num_inference_steps)
+        self.ts = scheduler.timesteps.to(torch.int32).to(dev)
+        self.coef = scheduler.coef_table(dev)
+        F_, R, h, Bu, P = self.F, self.R, self.h, self.Bu, self.P
+        cd = unet.config.cross_attention_dim
+        z = lambda *s, dt=torch.bfloat16: torch.zeros(s, dtype=dt, device=dev)
+        self.faces = z(F_, 3, R, R, dt=torch.uint8)
+        self.mask = z(R, R, dt=torch.float32)
+        self.audio = z(Bu * F_ * audio_tokens, cd)
+        self.init_lat = z(P, 4, dt=torch.float32)
+        self.eps_m = z(P, 4, dt=torch.float32)
+        self.eps_r = z(P, 4, dt=torch.float32)
+        self.lat = z(P, 4, dt=torch.float32)
+        self.cond = z(P, 16)
+        self.unet_in = z(Bu * F_, h, h, self.ud.cin_pad)
+        self.step = z(1, dt=torch.int32)
+        self.pix = z(F_, R, R, 8)
+        self.masked = z(F_, R, R, 8)
+        self.zdec = z(F_, h, h, 8)
+        self.out = z(F_, 3, R, R, dt=torch.float32)
+        self.out_u8 = z(F_, R, R, 3, dt=torch.uint8)
+        self.use_graphs = use_graphs
+        self.graphs = None
+
+    # -- the three phases --------------------------------------------------------
+    def _encode(self):
+        ops.prep_pixels(self.faces, self.mask, 8, self.pix, self.masked)
+        mom = self.vd.encode_moments(self.masked)
+        ops.vae_sample(mom, self.eps_m, SCALING, 0.0, self.cond, 5)
+        mom = self.vd.encode_moments(self.pix)
+        ops.vae_sample(mom, self.eps_r, SCALING, 0.0, self.cond, 9)
+        self.lat.copy_(self.init_lat)
+        ops.pack_unet_input(self.lat, self.cond, self.mask, self.F, self.R, self.h, self.Bu, self.unet_in)
+        self.step.zero_()
+
+    def _step(self):
+        eps = self.ud.forward(self.unet_in, self.Bu, self.ts, self.step, self.audio, self.L)
+        ops.ddim_cfg_step(eps, self.Bu, self.g, self.lat, self.coef, self.step, self.unet_in)
+
+    def _decode(self):
+        ops.scale_latents(self.lat, 1.0 / SCALING, 0.0, self.zdec)
+        dec = self.vd.decode(self.zdec)
+        ops.paste_back(dec, self.pix, self.mask, self.out, self.out_u8)
+
+    def capture(self):
+        """Warm up eagerly once, then capture the three phases as hipGraphs."""
+        self._encode()
+        self._step()
+        self._decode()
+        torch.cuda.synchronize(self.device)
+        pool = torch.cuda.graph_pool_handle()
+        graphs = []
+        for fn in (self._encode, self._step, self._decode):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                fn()
+            graphs.append(g)
+        torch.cuda.synchronize(self.device)
+        self.graphs = graphs
+
+    # -- inputs / execution -------------------------------------------------------
+    def load(self, faces_u8, mask, audio_chunks, init_latent, eps_masked, eps_ref):
+        """Stage one window's inputs into the static device buffers.
+        faces (F,3,R,R) uint8; mask (R,R) keep-mask; audio (F,50,384);
+        init_latent (1,4,1,h,w) or (1,4,F,h,w); eps_* (F,4,h,w)."""
+        F_, h = self.F, self.h
+        self.faces.copy_(faces_u8)
+        self.mask.copy_(mask)
+        a = audio_chunks.reshape(F_ * self.L, -1).to(torch.bfloat16)
+        if self.Bu == 2:  # torch.cat([zeros, audio]) (lipsync_pipeline.py:505-507)
+            self.audio[: F_ * self.L].zero_()
+            self.audio[F_ * self.L:].copy_(a)
+        else:
+            self.audio.copy_(a)
+        il = init_latent.float()
+        if il.shape[2] == 1:
+            il = il.expand(1, 4, F_, h, h)
+        self.init_lat.copy_(il[0].permute(1, 2, 3, 0).reshape(-1, 4))
+        self.eps_m.copy_(eps_masked.float().permute(0, 2, 3, 1).reshape(-1, 4))
+        self.eps_r.copy_(eps_ref.float().permute(0, 2, 3, 1).reshape(-1, 4))
+
+    def run(self):
+        """Execute the staged window; results in self.out (F,3,R,R) fp32 and
+        self.out_u8 (F,R,R,3)."""
+        if self.use_graphs:
+            if self.graphs is None:
+                self.capture()
+            g_enc, g_step, g_dec = self.graphs
+            g_enc.replay()
+            for _ in range(self.steps):
+                g_step.replay()
+            g_dec.replay()
+        else:
+            self._encode()
+            for _ in range(self.steps):
+                self._step()
+            self._decode()
+        return self.out
+
+
+# --------------------------------------------------------------------------
+# pipeline (reference API)
+# --------------------------------------------------------------------------
+
+
+class LipsyncPipeline:
+    """Drop-in for LipsyncPipeline(vae, audio_encoder, denoising_unet, scheduler)."""
+
+    def __init__(self, vae, audio_encoder, denoising_unet, scheduler):
+        if hasattr(scheduler.config, "steps_offset") and scheduler.config.steps_offset != 1:
+            scheduler.config["steps_offset"] = 1  # :65-77
+        if hasattr(scheduler.config, "clip_sample") and scheduler.config.clip_sample is True:
+            scheduler.config["clip_sample"] = False  # :79-90
+        self.vae, self.audio_encoder, self.denoising_unet, self.scheduler = vae, audio_encoder, denoising_unet, scheduler
+        self.vae_scale_factor = 2 ** (len(self.vae.config.block_out_channels) - 1)
+        self._engines = {}
+
+    @property
+    def device(self):
+        return self.denoising_unet.device
+
+    def to(self, device):
+        self.vae.to(device)
+        self.denoising_unet.to(device)
+        if self.audio_encoder is not None and hasattr(self.audio_encoder, "to"):
+            self.audio_encoder.to(device)
+        return self
+
+    def check_inputs(self, height, width, callback_steps):
+        assert height == width, "Height and width must be equal"
+        if height % 8 != 0 or width % 8 != 0:
+            raise ValueError(f"`height` and `width` have to be divisible by 8 but are {height} and {width}.")
+        if callback_steps is None or not isinstance(callback_steps, int) or callback_steps <= 0:
+            raise ValueError(f"`callback_steps` has to be a positive integer but is {callback_steps} of type"
+                             f" {type(callback_steps)}.")
+
+    def engine(self, num_frames, resolution, steps, guidance_scale, use_graphs=True):
+        key = (num_frames, resolution, steps, float(guidance_scale), use_graphs)
+        if key not in self._engines:
+            self._engines[key] = WindowEngine(self.denoising_unet, self.vae, self.scheduler, num_frames, resolution,
+                                              steps, guidance_scale, use_graphs)
+        return self._engines[key]
+
+    def prepare_latents(self, num_frames, height, width, generator=None):
+        """:182-196 -- one (1,4,1,h,w) draw repeated over every frame."""
+        shape = (1, self.vae.config.latent_channels, 1, height // self.vae_scale_factor,
+                 width // self.vae_scale_factor)
+        lat = torch.randn(shape, generator=generator, device=self.device, dtype=torch.float32)
+        return lat.repeat(1, 1, num_frames, 1, 1) * self.scheduler.init_noise_sigma
+
+    def run_windows(self, faces_u8, whisper_chunks, mask, num_frames=16, num_inference_steps=20, guidance_scale=1.5,
+                    generator=None, all_latents=None, vae_noise=None, callback=None, callback_steps=1):
+        """The hot loop (:489-575) over ceil(len(chunks)/num_frames) windows.
+        faces_u8 (N,3,R,R) (N >= #chunks, already repeated/truncated as the
+        reference does), whisper_chunks (N,50,384).  Returns decoded + pasted
+        frames (N', 3, R, R) fp32 and uint8 (N', R, R, 3) on device."""
+        R = faces_u8.shape[-1]
+        self.check_inputs(R, R, callback_steps)
+        n = whisper_chunks.shape[0]
+        if all_latents is None:
+            all_latents = self.prepare_latents(n, R, R, generator)
+        eng = self.engine(num_frames, R, num_inference_steps, guidance_scale)
+        h = R // self.vae_scale_factor
+        outs, outs_u8 = [], []
+        mask = mask.to(self.device, torch.float32)
+        n_inf = math.ceil(n / num_frames)
+        for i in range(n_inf):
+            sl = slice(i * num_frames, (i + 1) * num_frames)
+            fw = faces_u8[sl].to(self.device)
+            if fw.shape[0] != num_frames:
+                raise ValueError("the last window is short: pad the chunks to a multiple of num_frames "
+                                 "(pad_whisper_chunks_end, as the reference does)")
+            if vae_noise is not None:
+                em, er = vae_noise(i)
+            else:
+                em = torch.randn((num_frames, 4, h, h), generator=generator, device=self.device)
+                er = torch.randn((num_frames, 4, h, h), generator=generator, device=self.device)
+            eng.load(fw, mask, whisper_chunks[sl].to(self.device), all_latents[:, :, sl], em, er)
+            eng.run()
+            outs.append(eng.out.clone())
+            outs_u8.append(eng.out_u8.clone())
+            if callback is not None:
+                callback(i, None, eng.lat)
+        return torch.cat(outs), torch.cat(outs_u8)
+
+    @torch.no_grad()
+    def __call__(self, video_path, audio_path, video_out_path, video_mask_path=None, num_frames=16, video_fps=25,
+                 audio_sample_rate=16000, height=None, width=None, num_inference_steps=20, guidance_scale=1.5,
+                 weight_dtype=torch.float16, eta=0.0, mask="fix_mask", mask_image_path="latentsync/utils/mask.png",
+                 generator=None, callback=None, callback_steps=1, data_path=None, start_from_backwards=False,
+                 force_video_length=False, use_darken=False, brightness_factor=1.0, **kwargs):
+        """:360-604.  Face alignment, restore_video (cv2 warp-back) and ffmpeg
+        muxing are CPU I/O outside this build's scope; the
+        precomputed ``data_path`` (.pth {faces, boxes, affine_matrices}) is the
+        supported face source and the output is written as an .npz of the
+        lip-synced face frames (uint8) plus the aligned audio."""
+        from . import repeat as rep
+        if eta != 0.0:
+            raise NotImplementedError("eta > 0")
+        if mask != "fix_mask":
+            raise NotImplementedError("only mask='fix_mask' is on the inference path")
+        if not data_path:
+            raise NotImplementedError("face detection / alignment is out of scope: pass data_path (.pth)")
+        data = torch.load(data_path, map_location="cpu", weights_only=True)
+        faces = data["faces"]
+        R = height or faces.shape[-1]
+        self.check_inputs(R, width or R, callback_steps)
+        if faces.shape[-1] != R:
+            raise NotImplementedError("face resize needs torchvision (out of scope): store faces at the resolution")
+        keep = load_fixed_mask(R, mask_image_path)
+        audio_samples = self.audio_encoder.read_audio(audio_path, audio_sample_rate)
+        feat = self.audio_encoder.audio2feat(audio_path)
+        chunks = self.audio_encoder.feature2chunks(feature_array=feat, fps=video_fps)
+        shape = chunks[0].shape
+        padding_duration = 0.0
+        if not force_video_length:
+            if start_from_backwards:
+                chunks, audio_samples, padding_duration, _ = rep.pad_whisper_chunks(chunks, shape, audio_samples,
+                                                                                     audio_sample_rate, video_fps)
+            else:
+                chunks, audio_samples, padding_duration = rep.pad_whisper_chunks_end(chunks, shape, audio_samples,
+                                                                                     audio_sample_rate, video_fps)
+            if len(chunks) > len(faces):
+                faces = rep.repeat_to_length(faces, len(chunks))
+        else:
+            chunks, audio_samples, padding_duration = rep.pad_whisper_chunks_to_target(
+                chunks, shape, audio_samples, audio_sample_rate, len(faces), fps=video_fps)
+        if len(faces) != len(chunks) and start_from_backwards:
+            faces = rep.truncate_to_length(faces, len(chunks))
+        chunks = torch.stack([c.to(self.device) for c in chunks])
+        out, out_u8 = self.run_windows(faces, chunks, keep, num_frames, num_inference_steps, guidance_scale,
+                                       generator, callback=callback, callback_steps=callback_steps)
+        n_out = out_u8.shape[0]
+        audio_keep = int(n_out / video_fps * audio_sample_rate)
+        np.savez(video_out_path if video_out_path.endswith(".npz") else video_out_path + ".npz",
+                 frames=out_u8.cpu().numpy(), audio=np.asarray(audio_samples[:audio_keep]),
+                 fps=video_fps, sample_rate=audio_sample_rate, padding_duration=padding_duration)
+        return None

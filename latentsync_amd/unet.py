@@ -399,11 +399,9 @@ class UNet3DConditionModel(torch.nn.Module):
         self.add_audio_layer = cfg["add_audio_layer"]
         self._shapes = unet_param_shapes(cfg)
         # reference __init__ draws nn defaults; weights here come from the
-        # deterministic generator until a checkpoint is loaded.
-        self._sd = fill_state_dict(self._shapes, 0)
-        for k in self._shapes:
-            if k.endswith("pos_encoder.pe"):
-                self._sd[k] = positional_encoding(self._shapes[k][-1], self._shapes[k][1])[None]
+        # deterministic generator (seed 0, drawn lazily) until a checkpoint is
+        # loaded or init_weights(seed) is called.
+        self._sd_store = None
         self._device = torch.device("cpu")
         self._dev = None
         self.num_upsamplers = len(cfg["block_out_channels"]) - 1
@@ -431,6 +429,13 @@ class UNet3DConditionModel(torch.nn.Module):
         return None
 
     # -- weights ------------------------------------------------------------
+    @property
+    def _sd(self):
+        if self._sd_store is None:
+            self._sd_store = {}
+            self.init_weights(0, _pack=False)
+        return self._sd_store
+
     def state_dict(self, *a, **k):
         return dict(self._sd)
 
@@ -471,13 +476,15 @@ class UNet3DConditionModel(torch.nn.Module):
             unet.load_state_dict(ckpt["state_dict"], strict=False)
         return unet.to(device), step
 
-    def init_weights(self, seed: int):
+    def init_weights(self, seed: int, _pack=True):
         """Deterministic reference-independent weights (latentsync_amd.weights)."""
         sd = fill_state_dict(self._shapes, seed)
-        for k, v in sd.items():
-            self._sd[k] = v
+        for k in self._shapes:
+            if k.endswith("pos_encoder.pe"):
+                sd[k] = positional_encoding(self._shapes[k][-1], self._shapes[k][1])[None]
+        self._sd_store = sd
         self._dev = None
-        if self._device.type == "cuda":
+        if _pack and self._device.type == "cuda":
             self._pack()
         return self
 

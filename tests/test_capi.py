@@ -49,5 +49,5 @@ def test_attention_validation():
     lib = _lib.load()
     d = _lib.AttnDesc()
     d.q = d.k = d.v = d.o = 16
-    d.batch, d.z2, d.heads, d.nq, d.nk, d.head_dim = 1, 1, 1, 16, 16, 44
+    d.batch, d.z2, d.heads, d.nq, d.nk, d.head_dim = 1, 1, 1, 16, 16, 513
     assert lib.ls_attention(C.byref(d), None) == 1

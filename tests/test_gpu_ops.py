@@ -151,7 +151,7 @@ def _sdpa(q, k, v, scale=None):
 
 @pytest.mark.parametrize("n,N,Nk,heads,d", [(4, 256, 256, 8, 40), (2, 64, 64, 8, 80), (2, 16, 16, 8, 160),
                                             (3, 256, 50, 8, 40), (2, 64, 50, 8, 160), (1, 100, 100, 6, 64),
-                                            (2, 64, 64, 1, 512), (2, 1024, 1024, 1, 128)])
+                                            (2, 64, 64, 1, 512), (2, 1024, 1024, 1, 128), (2, 64, 64, 8, 4)])
 def test_attention_spatial(gpu, n, N, Nk, heads, d):
     C = heads * d
     q = bf(rnd(n, N, C, seed=50))
