@@ -89,18 +89,12 @@ class _Dev:
         b = (self.sd.get(bkey) if bkey else None) if b is None else b
         if ksize is None:
             ksize = w.shape[-1] if w.dim() == 4 else 1
-        n_out = w.shape[0]
+        n_out = max(w.shape[0], n_pad or 0)  # padded output channels are written as zeros
         if geglu:
             w, b = geglu_interleave(w.float(), b.float())
         wp = pack_weight(w, cin_pad=cin_pad, n_pad=n_pad)
         bp = pad_bias(b, n_pad)
-        cin = wp.shape[1] // (ksize * ksize) if ksize == 1 else None
-        if ksize == 3:
-            i = w.shape[1]
-            cin = cin_pad or (i + 7) // 8 * 8
-        elif ksize == 1:
-            i = w.shape[1]
-            cin = cin_pad or (i + 7) // 8 * 8
+        cin = cin_pad or (w.shape[1] + 7) // 8 * 8
         return ops.Packed(wp.to(torch.bfloat16).to(self.device).contiguous(),
                           None if bp is None else bp.to(self.device).contiguous(), cin, ksize, n_out, geglu)
 
@@ -255,10 +249,9 @@ class _DeviceUNet:
         self.boc = boc
         self.temb_dim = boc[0] * 4
         self.flip, self.shift = bool(cfg["flip_sin_to_cos"]), float(cfg["freq_shift"])
-        self.t1 = dv.packed("time_embedding.linear_1.weight")
-        self.t1b = dv.f32("time_embedding.linear_1.bias")
-        self.t2 = dv.packed("time_embedding.linear_2.weight")
-        self.t2b = dv.f32("time_embedding.linear_2.bias")
+        bfw = lambda k: sd[k].to(torch.bfloat16).to(device).contiguous()  # ls_small_linear: plain [N][K]
+        self.t1, self.t1b = bfw("time_embedding.linear_1.weight"), dv.f32("time_embedding.linear_1.bias")
+        self.t2, self.t2b = bfw("time_embedding.linear_2.weight"), dv.f32("time_embedding.linear_2.bias")
         self.conv_in = dv.packed("conv_in.weight", "conv_in.bias", cin_pad=self.cin_pad)
         temb_w, temb_b = [], []
 
@@ -320,8 +313,8 @@ class _DeviceUNet:
 
     def temb(self, ts_i32, step_i32, B):
         t = ops.timestep_embed(ts_i32, step_i32, B, self.boc[0], self.flip, self.shift)
-        e1 = ops.small_linear(t, self.t1.w, self.t1b)
-        emb = ops.small_linear(e1, self.t2.w, self.t2b, silu_in=True)
+        e1 = ops.small_linear(t, self.t1, self.t1b)
+        emb = ops.small_linear(e1, self.t2, self.t2b, silu_in=True)
         return ops.small_linear(emb, self.temb_w, self.temb_b, silu_in=True)
 
     def forward(self, x_in, B, ts_i32, step_i32, audio_rows, n_audio_tok, down_res=None, mid_res=None):
