@@ -97,16 +97,21 @@ size_t ls_conv_workspace_bytes(const ls_conv_desc* d);
  * motion_module.py:101) and the SD-VAE GroupNorms.
  * Input: n_samples * pix_per_sample pixels of C = C1 + C2 channels (x2 = concat).
  * Output: scale[s, c] = gamma[c] * rstd[s, g]; shift[s, c] = beta[c] - mean[s, g] * scale.
- * workspace >= ls_groupnorm_workspace_bytes().
+ * One launch: the last-arriving block of a sample merges the split partials.
+ * workspace >= ls_groupnorm_workspace_bytes(); its first 4 KiB are arrival
+ * counters that must be zero before the first call (each call re-arms them).
  */
 int ls_groupnorm(const uint16_t* x1, const uint16_t* x2, int32_t C1, int32_t C2, int32_t n_samples,
                  int64_t pix_per_sample, int32_t groups, float eps, const float* gamma, const float* beta,
                  float* scale, float* shift, void* workspace, size_t workspace_bytes, void* stream);
 size_t ls_groupnorm_workspace_bytes(int32_t n_samples, int32_t groups);
 
-/* Materialised GroupNorm(+SiLU) apply (used where the consumer is not a GEMM). */
-int ls_affine_act(const uint16_t* x, int64_t n_pix, int32_t C, int64_t pix_per_sample, const float* scale,
-                  const float* shift, int32_t silu, uint16_t* y, void* stream);
+/* Materialised GroupNorm(+SiLU) apply over an optional channel concat
+ * (x1 | x2) -> y [n_pix][C1 + C2]: the input of a 3x3 conv, whose gather would
+ * otherwise recompute the affine + SiLU once per tap and per N-tile. */
+int ls_groupnorm_apply(const uint16_t* x1, const uint16_t* x2, int32_t C1, int32_t C2, int64_t n_pix,
+                       int64_t pix_per_sample, const float* scale, const float* shift, int32_t silu, uint16_t* y,
+                       void* stream);
 
 /*
  * LayerNorm over the last dim (nn.LayerNorm of BasicTransformerBlock

@@ -53,7 +53,8 @@ _SIGS = {
     "ls_groupnorm": (C.c_int, [c_vp, c_vp, C.c_int32, C.c_int32, C.c_int32, C.c_int64, C.c_int32, C.c_float,
                                c_vp, c_vp, c_vp, c_vp, c_vp, C.c_size_t, c_vp]),
     "ls_groupnorm_workspace_bytes": (C.c_size_t, [C.c_int32, C.c_int32]),
-    "ls_affine_act": (C.c_int, [c_vp, C.c_int64, C.c_int32, C.c_int64, c_vp, c_vp, C.c_int32, c_vp, c_vp]),
+    "ls_groupnorm_apply": (C.c_int, [c_vp, c_vp, C.c_int32, C.c_int32, C.c_int64, C.c_int64, c_vp, c_vp, C.c_int32,
+                                     c_vp, c_vp]),
     "ls_layernorm": (C.c_int, [c_vp, C.c_int64, C.c_int32, C.c_float, c_vp, c_vp, c_vp, C.c_int32, C.c_int32,
                                c_vp, c_vp]),
     "ls_attention": (C.c_int, [C.POINTER(AttnDesc), c_vp]),

@@ -30,39 +30,86 @@ struct ConvArgs {
 };
 
 // ---------------------------------------------------------------- epilogue
-__device__ __forceinline__ float epi_value(const ConvArgs& a, int row, int col, float v) {
-  if (a.bias) v += a.bias[col];
-  if (a.rowvec) v += a.rowvec[(long)(row / a.rows_per_vec) * a.rowvec_ld + col];
-  if (a.res) v += bf2f(a.res[(long)row * a.ldr + col]);
-  v *= a.out_scale;
-  if (a.act == LS_ACT_GELU) v = gelu_erf(v);
-  else if (a.act == LS_ACT_SILU) v = silu(v);
+// Vectorised epilogue on 8 consecutive output columns (16-B bf16 / 32-B fp32
+// stores).  All global loads of a chunk are issued before its stores.
+struct Chunk8 { float v[8]; };
+
+__device__ __forceinline__ void load8f(const float* __restrict__ p, float* d) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+}
+
+__device__ __forceinline__ float act_fn(int act, float v) {
+  if (act == LS_ACT_GELU) return gelu_erf(v);
+  if (act == LS_ACT_SILU) return silu(v);
   return v;
 }
 
-__device__ __forceinline__ void epi_store(const ConvArgs& a, int row, int col, float v) {
-  if (a.y_f32) ((float*)a.y)[(long)row * a.ldy + col] = v;
-  else ((u16*)a.y)[(long)row * a.ldy + col] = f2bf(v);
+// v[8] = accumulators of packed columns [col, col+8) of `row`; applies bias,
+// rowvec, residual, scale, activation and stores.  vec = all 8 in range and aligned.
+__device__ __forceinline__ void epi_chunk(const ConvArgs& a, int row, int col, float* v, bool vec) {
+  if (row >= a.M) return;
+  if (vec) {
+    float b[8], rv[8], rs[8];
+    if (a.bias) load8f(a.bias + col, b); else for (int j = 0; j < 8; ++j) b[j] = 0.f;
+    if (a.rowvec) load8f(a.rowvec + (long)(row / a.rows_per_vec) * a.rowvec_ld + col, rv);
+    else for (int j = 0; j < 8; ++j) rv[j] = 0.f;
+    if (a.res) unpack8(*(const uint4*)(a.res + (long)row * a.ldr + col), rs);
+    else for (int j = 0; j < 8; ++j) rs[j] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = act_fn(a.act, (v[j] + b[j] + rv[j] + rs[j]) * a.out_scale);
+    if (a.y_f32) {
+      float* y = (float*)a.y + (long)row * a.ldy + col;
+      *(float4*)y = make_float4(v[0], v[1], v[2], v[3]);
+      *(float4*)(y + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    } else {
+      *(uint4*)((u16*)a.y + (long)row * a.ldy + col) = pack8(v);
+    }
+  } else {
+    for (int j = 0; j < 8; ++j) {
+      const int c = col + j;
+      if (c >= a.N) break;
+      float t = v[j];
+      if (a.bias) t += a.bias[c];
+      if (a.rowvec) t += a.rowvec[(long)(row / a.rows_per_vec) * a.rowvec_ld + c];
+      if (a.res) t += bf2f(a.res[(long)row * a.ldr + c]);
+      t = act_fn(a.act, t * a.out_scale);
+      if (a.y_f32) ((float*)a.y)[(long)row * a.ldy + c] = t;
+      else ((u16*)a.y)[(long)row * a.ldy + c] = f2bf(t);
+    }
+  }
 }
 
-// GEGLU: packed column 32b+i holds h_{16b+i}, 32b+16+i holds g_{16b+i}.
-__device__ __forceinline__ void epi_geglu(const ConvArgs& a, int row, int pcol_h, float h, float g) {
-  if (a.bias) { h += a.bias[pcol_h]; g += a.bias[pcol_h + 16]; }
-  const int ocol = (pcol_h >> 5) * 16 + (pcol_h & 15);
-  epi_store(a, row, ocol, h * gelu_erf(g));
+// GEGLU chunk: h[8] = packed cols [ph, ph+8), g[8] = [ph+16, ph+24) -> out cols [oc, oc+8)
+__device__ __forceinline__ void epi_geglu8(const ConvArgs& a, int row, int ph, float* h, const float* g, bool vec) {
+  if (row >= a.M) return;
+  const int oc = (ph >> 5) * 16 + (ph & 15);
+  float bh[8], bg[8];
+  if (a.bias) { load8f(a.bias + ph, bh); load8f(a.bias + ph + 16, bg); }
+  else for (int j = 0; j < 8; ++j) { bh[j] = 0.f; bg[j] = 0.f; }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) h[j] = (h[j] + bh[j]) * gelu_erf(g[j] + bg[j]);
+  if (vec && !a.y_f32) *(uint4*)((u16*)a.y + (long)row * a.ldy + oc) = pack8(h);
+  else
+    for (int j = 0; j < 8; ++j) {
+      if (a.y_f32) ((float*)a.y)[(long)row * a.ldy + oc + j] = h[j];
+      else ((u16*)a.y)[(long)row * a.ldy + oc + j] = f2bf(h[j]);
+    }
 }
 
 // ---------------------------------------------------------------- A gather
+// Per-row geometry precomputed once per thread: pixel base of the image, and
+// the top-left input coordinate of the 3x3 window (or a sentinel for m >= M).
+struct RowGeo { int pb, yb, xb; };
+
 template <int KS, bool TAPU>
-__device__ __forceinline__ uint4 load_a_chunk(const ConvArgs& a, int kt, int ch, int m, int n, int yo, int xo) {
-  if (m >= a.M) return make_uint4(0, 0, 0, 0);
-  int c, tap;
+__device__ __forceinline__ uint4 load_a_chunk(const ConvArgs& a, int kt, int ch, int m, const RowGeo& g) {
+  int c, tap = 0;
   if (KS == 1) {
-    tap = 0;
     c = kt * 64 + ch * 8;
-    if (c >= a.Cin) return make_uint4(0, 0, 0, 0);
+    if (m >= a.M || c >= a.Cin) return make_uint4(0, 0, 0, 0);
   } else if (TAPU) {
-    tap = (kt * 64) / a.Cin;  // uniform across the tile
+    tap = (kt * 64) / a.Cin;
     c = kt * 64 - tap * a.Cin + ch * 8;
   } else {
     const int kc = kt * 8 + ch;
@@ -75,31 +122,27 @@ __device__ __forceinline__ uint4 load_a_chunk(const ConvArgs& a, int kt, int ch,
     pix = m;
   } else {
     const int kh = tap / 3, kw = tap - kh * 3;
-    int yy = yo * a.stride + kh - a.pad;
-    int xx = xo * a.stride + kw - a.pad;
+    int yy = g.yb + kh, xx = g.xb + kw;
     if (a.upsample) {
-      if (yy < 0 || xx < 0 || yy >= 2 * a.H || xx >= 2 * a.W) return make_uint4(0, 0, 0, 0);
+      if ((unsigned)yy >= (unsigned)(2 * a.H) || (unsigned)xx >= (unsigned)(2 * a.W)) return make_uint4(0, 0, 0, 0);
       yy >>= 1; xx >>= 1;
     } else {
-      if (yy < 0 || xx < 0 || yy >= a.H || xx >= a.W) return make_uint4(0, 0, 0, 0);
+      if ((unsigned)yy >= (unsigned)a.H || (unsigned)xx >= (unsigned)a.W) return make_uint4(0, 0, 0, 0);
     }
-    pix = ((long)n * a.H + yy) * a.W + xx;
+    pix = (long)g.pb + yy * a.W + xx;
   }
   uint4 v;
   if (c < a.C1) v = *(const uint4*)(a.x1 + pix * a.ld1 + c);
   else v = *(const uint4*)(a.x2 + pix * a.ld2 + (c - a.C1));
   if (a.aff_scale) {
     const long s = pix / a.pix_per_sample;
-    const float4* sc = (const float4*)(a.aff_scale + s * a.Cin + c);
-    const float4* sh = (const float4*)(a.aff_shift + s * a.Cin + c);
-    const float4 s0 = sc[0], s1 = sc[1], h0 = sh[0], h1 = sh[1];
-    const float scl[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-    const float shf[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-    float f[8];
+    float scl[8], shf[8], f[8];
+    load8f(a.aff_scale + s * a.Cin + c, scl);
+    load8f(a.aff_shift + s * a.Cin + c, shf);
     unpack8(v, f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float t = f[j] * scl[j] + shf[j];
+      const float t = f[j] * scl[j] + shf[j];
       f[j] = a.silu_in ? silu(t) : t;
     }
     v = pack8(f);
@@ -114,6 +157,8 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvArgs a) {
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int FM = WTM / 16, FN = WTN / 16;
   constexpr int AL = BM / 32, BL = BN / 32;  // 16-B chunks per thread per K-tile
+  constexpr int SP = BN + 4;                 // epilogue staging pitch (floats)
+  static_assert(WTM * SP * 4 <= 2 * (BM + BN) * 8 * 16, "staging must fit the LDS ring");
   __shared__ uint4 lds[2][(BM + BN) * 8];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -127,9 +172,9 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvArgs a) {
   const int kt0 = z * a.kt_per_split;
   const int kt1 = min(a.ktiles, kt0 + a.kt_per_split);
 
-  // per-thread fixed A rows
   const int ch = tid & 7;
-  int rm[AL], rn[AL], ryo[AL], rxo[AL];
+  int rm[AL];
+  RowGeo geo[AL];
 #pragma unroll
   for (int i = 0; i < AL; ++i) {
     const int m = m0 + (tid >> 3) + 32 * i;
@@ -137,16 +182,19 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvArgs a) {
     if (KS == 3) {
       const int hw = a.Ho * a.Wo;
       const int n = m / hw, r = m - n * hw;
-      rn[i] = n; ryo[i] = r / a.Wo; rxo[i] = r - ryo[i] * a.Wo;
+      const int yo = r / a.Wo, xo = r - yo * a.Wo;
+      geo[i].pb = n * a.H * a.W;
+      geo[i].yb = (m < a.M) ? (a.upsample ? yo - a.pad : yo * a.stride - a.pad) : -(1 << 28);
+      geo[i].xb = a.upsample ? xo - a.pad : xo * a.stride - a.pad;
     } else {
-      rn[i] = 0; ryo[i] = 0; rxo[i] = 0;
+      geo[i].pb = 0; geo[i].yb = 0; geo[i].xb = 0;
     }
   }
 
   uint4 ra[AL], rb[BL];
   auto gload = [&](int kt) {
 #pragma unroll
-    for (int i = 0; i < AL; ++i) ra[i] = load_a_chunk<KS, TAPU>(a, kt, ch, rm[i], rn[i], ryo[i], rxo[i]);
+    for (int i = 0; i < AL; ++i) ra[i] = load_a_chunk<KS, TAPU>(a, kt, ch, rm[i], geo[i]);
 #pragma unroll
     for (int j = 0; j < BL; ++j) {
       const int n = n0 + (tid >> 3) + 32 * j;
@@ -197,75 +245,128 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvArgs a) {
   }
 
   // ---------------------------------------------------------------- epilogue
-  const int rbase = m0 + wm * WTM + (lane >> 4) * 4;
-  const int cbase = n0 + wn * WTN + (lane & 15);
-  if (a.split > 1) {
-    float* P = a.partial + (long)z * a.M * a.N;
+  // Stage the tile through LDS one wave-row (WTM rows) at a time, then each
+  // thread handles whole 8-column chunks.
+  float* st = (float*)&lds[0][0];
+  const bool vec = (a.N % 8 == 0) && (a.ldy % 8 == 0) && (!a.res || a.ldr % 8 == 0);
+  const bool geglu = a.act == LS_ACT_GEGLU;
+#pragma unroll 1
+  for (int p = 0; p < WM; ++p) {
+    if (wm == p) {
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
+        for (int j = 0; j < FN; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = rbase + i * 16 + r, col = cbase + j * 16;
-          if (row < a.M && col < a.N) P[(long)row * a.N + col] = acc[i][j][r];
+          for (int r = 0; r < 4; ++r)
+            st[(i * 16 + (lane >> 4) * 4 + r) * SP + wn * WTN + j * 16 + (lane & 15)] = acc[i][j][r];
+    }
+    __syncthreads();
+    const int rbase = m0 + p * WTM;
+    if (a.split > 1) {
+      float* P = a.partial + (long)z * a.M * a.N;
+      for (int q = tid; q < WTM * (BN / 8); q += 256) {
+        const int r = q / (BN / 8), c8 = (q - r * (BN / 8)) * 8;
+        const int row = rbase + r, col = n0 + c8;
+        if (row >= a.M || col >= a.N) continue;
+        const float* s = st + r * SP + c8;
+        if (vec) {
+          *(float4*)(P + (long)row * a.N + col) = *(const float4*)s;
+          *(float4*)(P + (long)row * a.N + col + 4) = *(const float4*)(s + 4);
+        } else {
+          for (int j = 0; j < 8 && col + j < a.N; ++j) P[(long)row * a.N + col + j] = s[j];
         }
-    return;
-  }
-  if (a.act == LS_ACT_GEGLU) {
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; j += 2)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = rbase + i * 16 + r, col = cbase + j * 16;
-          if (row < a.M && col < a.N) epi_geglu(a, row, col, acc[i][j][r], acc[i][j + 1][r]);
-        }
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = rbase + i * 16 + r, col = cbase + j * 16;
-        if (row < a.M && col < a.N) epi_store(a, row, col, epi_value(a, row, col, acc[i][j][r]));
       }
+    } else if (geglu) {
+      for (int q = tid; q < WTM * (BN / 16); q += 256) {
+        const int r = q / (BN / 16), o8 = (q - r * (BN / 16)) * 8;
+        const int ph = (o8 >> 4) * 32 + (o8 & 15);
+        const int row = rbase + r, col = n0 + ph;
+        if (col >= a.N) continue;
+        float h[8], g[8];
+        const float* s = st + r * SP + ph;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { h[j] = s[j]; g[j] = s[16 + j]; }
+        epi_geglu8(a, row, col, h, g, vec);
+      }
+    } else {
+      for (int q = tid; q < WTM * (BN / 8); q += 256) {
+        const int r = q / (BN / 8), c8 = (q - r * (BN / 8)) * 8;
+        const int row = rbase + r, col = n0 + c8;
+        if (col >= a.N) continue;
+        float v[8];
+        const float* s = st + r * SP + c8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = s[j];
+        epi_chunk(a, row, col, v, vec && col + 8 <= a.N);
+      }
+    }
+    __syncthreads();
+  }
 }
 
-// split-K reduction + epilogue: one thread per output element
+// split-K reduction + epilogue: one thread per 8 output columns
 __global__ void splitk_reduce_kernel(ConvArgs a) {
-  const int nout = (a.act == LS_ACT_GEGLU) ? a.N / 2 : a.N;
+  const bool geglu = a.act == LS_ACT_GEGLU;
+  const int nout = geglu ? a.N / 2 : a.N;
+  const int cpr = (nout + 7) / 8;
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (long)a.M * nout) return;
-  const int row = idx / nout, oc = idx - (long)row * nout;
+  if (idx >= (long)a.M * cpr) return;
+  const int row = idx / cpr, o8 = (int)(idx - (long)row * cpr) * 8;
   const long MN = (long)a.M * a.N;
-  if (a.act == LS_ACT_GEGLU) {
-    const int ph = (oc >> 4) * 32 + (oc & 15);
-    float h = 0.f, g = 0.f;
+  const bool vec = (a.N % 8 == 0) && (a.ldy % 8 == 0) && (!a.res || a.ldr % 8 == 0);
+  if (geglu) {
+    const int ph = (o8 >> 4) * 32 + (o8 & 15);
+    float h[8], g[8], t[8];
+    for (int j = 0; j < 8; ++j) { h[j] = 0.f; g[j] = 0.f; }
     for (int z = 0; z < a.split; ++z) {
-      h += a.partial[z * MN + (long)row * a.N + ph];
-      g += a.partial[z * MN + (long)row * a.N + ph + 16];
+      load8f(a.partial + z * MN + (long)row * a.N + ph, t);
+      for (int j = 0; j < 8; ++j) h[j] += t[j];
+      load8f(a.partial + z * MN + (long)row * a.N + ph + 16, t);
+      for (int j = 0; j < 8; ++j) g[j] += t[j];
     }
-    epi_geglu(a, row, ph, h, g);
+    epi_geglu8(a, row, ph, h, g, vec);
   } else {
-    float v = 0.f;
-    for (int z = 0; z < a.split; ++z) v += a.partial[z * MN + (long)row * a.N + oc];
-    epi_store(a, row, oc, epi_value(a, row, oc, v));
+    float v[8];
+    for (int j = 0; j < 8; ++j) v[j] = 0.f;
+    for (int z = 0; z < a.split; ++z) {
+      const float* p = a.partial + z * MN + (long)row * a.N + o8;
+      if (vec) {
+        float t[8];
+        load8f(p, t);
+        for (int j = 0; j < 8; ++j) v[j] += t[j];
+      } else {
+        for (int j = 0; j < 8 && o8 + j < a.N; ++j) v[j] += p[j];
+      }
+    }
+    epi_chunk(a, row, o8, v, vec && o8 + 8 <= a.N);
   }
 }
 
 // ---------------------------------------------------------------- host side
-struct TileCfg { int bm, bn; };
+struct TileCfg { int bm, bn, split; };
 
-static TileCfg pick_tile(long M, int N) {
-  if (N <= 32) return {128, 32};
-  const long t128 = (long)cdiv(M, 128) * cdiv(N, 128);
-  if (t128 >= 240) return {128, 128};
-  if ((long)cdiv(M, 128) * cdiv(N, 64) >= 240) return {128, 64};
-  return {64, 64};
+// Tile + split-K choice by a small cost model: time ~ max(1, blocks / CUs) x
+// per-block MFMA work / relative efficiency of the tile, + split-K slab traffic.
+static TileCfg pick_tile(long M, int N, int ktiles, bool allow_split) {
+  struct Cand { int bm, bn; double eff; };
+  const Cand cands[] = {{128, 128, 1.0}, {128, 64, 0.72}, {64, 64, 0.42}, {128, 32, 0.36}};
+  TileCfg best{128, 128, 1};
+  double best_t = 1e300;
+  for (const Cand& c : cands) {
+    if (c.bn == 32 && N > 32) continue;
+    if (N <= 32 && c.bn != 32) continue;
+    const long tiles = (long)cdiv(M, c.bm) * cdiv(N, c.bn);
+    for (int split = 1; split <= 16; split *= 2) {
+      if (split > 1 && (!allow_split || ktiles / split < 4)) break;
+      const long blocks = tiles * split;
+      const double per_block = (double)c.bm * c.bn * 64.0 * cdiv(ktiles, split) / c.eff;
+      double t = std::max(1.0, blocks / 256.0) * per_block;
+      if (split > 1) t += (double)M * N * split * 8.0;  // fp32 slab write + read: bytes at chip BW ~ MACs at CU rate
+      if (t < best_t * 0.97) { best_t = t; best = {c.bm, c.bn, split}; }
+    }
+  }
+  return best;
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -304,15 +405,9 @@ static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split
   a.res = d->res; a.ldr = d->ldr; a.out_scale = d->out_scale == 0.f ? 1.f : d->out_scale; a.act = d->act;
   a.y = d->y; a.ldy = d->ldy; a.y_f32 = d->y_f32;
   a.ktiles = d->K / 64;
-  t = pick_tile(M, d->N);
+  t = pick_tile(M, d->N, a.ktiles, d->split_k <= 0 && d->workspace != nullptr);
   a.ntm = cdiv(M, t.bm); a.ntn = cdiv(d->N, t.bn);
-  split = d->split_k;
-  if (split <= 0) {
-    split = 1;
-    const long tiles = (long)a.ntm * a.ntn;
-    if (tiles < 160 && a.ktiles >= 16) split = (int)std::min<long>(a.ktiles / 8, cdiv(320, tiles));
-    if (split < 1) split = 1;
-  }
+  split = d->split_k > 0 ? d->split_k : t.split;
   split = std::min(split, a.ktiles);
   a.kt_per_split = cdiv(a.ktiles, split);
   split = cdiv(a.ktiles, a.kt_per_split);
@@ -357,8 +452,8 @@ extern "C" int ls_conv2d(const ls_conv_desc* d, void* stream) {
   else launch_cfg<64, 64, 2, 2>(a, d->ksize, tapu, grid, s);
   if ((rc = check_launch("conv_gemm_kernel")) != LS_OK) return rc;
   if (a.split > 1) {
-    const long nout = (long)a.M * ((a.act == LS_ACT_GEGLU) ? a.N / 2 : a.N);
-    splitk_reduce_kernel<<<cdiv(nout, 256), 256, 0, s>>>(a);
+    const long nchunk = (long)a.M * ((((a.act == LS_ACT_GEGLU) ? a.N / 2 : a.N) + 7) / 8);
+    splitk_reduce_kernel<<<cdiv(nchunk, 256), 256, 0, s>>>(a);
     if ((rc = check_launch("splitk_reduce_kernel")) != LS_OK) return rc;
   }
   return LS_OK;

@@ -12,13 +12,38 @@
 namespace ls {
 
 constexpr int GN_THREADS = 256;
+constexpr size_t GN_COUNTER_BYTES = 4096;  // per-sample arrival tickets at the workspace start
 
 struct GnPart { double n, mean, m2, pad; };
 
+// Chan et al. merge of (n, mean, M2)
+__device__ __forceinline__ void chan_merge(double& n, double& mean, double& m2, double nb, double meanb, double m2b) {
+  if (nb <= 0) return;
+  const double nt = n + nb;
+  const double d = meanb - mean;
+  mean += d * nb / nt;
+  m2 += m2b + d * d * n * nb / nt;
+  n = nt;
+}
+
+__device__ __forceinline__ double shfl_xor_d(double v, int m) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __shfl_xor((int)(b & 0xffffffffLL), m, 64), hi = __shfl_xor((int)(b >> 32), m, 64);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// One launch: per-(split, sample) shifted partial sums -> per-group (n, mean, M2);
+// the LAST block of a sample (arrival ticket) merges the splits and writes the
+// per-channel affine.  Publication follows the agent-scope release/acquire
+// recipe (every storing wave drains vmcnt, barrier, lane-0 release fence,
+// ticket; the last arriver acquires before reading the partials).
 __global__ void __launch_bounds__(GN_THREADS)
-gn_partial_kernel(const u16* __restrict__ x1, const u16* __restrict__ x2, int C1, int C2, long pps, int nsplit,
-                  int groups, GnPart* __restrict__ part) {
-  extern __shared__ __attribute__((aligned(16))) float gsh[];  // [R][C] S1 then [R][C] S2 then k[C]
+gn_stats_kernel(const u16* __restrict__ x1, const u16* __restrict__ x2, int C1, int C2, long pps, int nsplit,
+                int groups, float eps, const float* __restrict__ gamma, const float* __restrict__ beta,
+                GnPart* part, unsigned* counters, float* __restrict__ scale, float* __restrict__ shift) {
+  extern __shared__ __attribute__((aligned(16))) float gsh[];  // [R][C] S1, [R][C] S2, k[C]
+  __shared__ float mean_s[64], rstd_s[64];
+  __shared__ int is_last;
   const int C = C1 + C2, CC = C / 8;
   const int split = blockIdx.x, s = blockIdx.y;
   const int tid = threadIdx.x;
@@ -38,27 +63,36 @@ gn_partial_kernel(const u16* __restrict__ x1, const u16* __restrict__ x2, int C1
     int cc, r;
     if (nchunk == 1) { cc = tid % CC; r = tid / CC; } else { cc = tid + q * GN_THREADS; r = 0; }
     const bool active = (nchunk == 1) ? (tid < R * CC) : (cc < CC);
+    if (!active) continue;
+    const int c = cc * 8;
     float a1[8], a2[8], k8[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { a1[j] = 0.f; a2[j] = 0.f; }
-    if (active) {
-      const int c = cc * 8;
+    for (int j = 0; j < 8; ++j) { a1[j] = 0.f; a2[j] = 0.f; k8[j] = kk[c + j]; }
+    const u16* src; int ld;
+    if (c < C1) { src = x1 + c; ld = C1; } else { src = x2 + (c - C1); ld = C2; }
+    long p = p0 + r;
+    for (; p + 3 * R < p1; p += 4 * R) {  // 4 loads in flight
+      uint4 u[4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) k8[j] = kk[c + j];
-      const u16* src; int ld;
-      if (c < C1) { src = x1 + c; ld = C1; } else { src = x2 + (c - C1); ld = C2; }
-      for (long p = p0 + r; p < p1; p += R) {
+      for (int t = 0; t < 4; ++t) u[t] = *(const uint4*)(src + (base + p + t * R) * ld);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
         float f[8];
-        unpack8(*(const uint4*)(src + (base + p) * ld), f);
+        unpack8(u[t], f);
 #pragma unroll
         for (int j = 0; j < 8; ++j) { const float d = f[j] - k8[j]; a1[j] += d; a2[j] += d * d; }
       }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { S1[(long)r * C + c + j] = a1[j]; S2[(long)r * C + c + j] = a2[j]; }
     }
+    for (; p < p1; p += R) {
+      float f[8];
+      unpack8(*(const uint4*)(src + (base + p) * ld), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { const float d = f[j] - k8[j]; a1[j] += d; a2[j] += d * d; }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { S1[(long)r * C + c + j] = a1[j]; S2[(long)r * C + c + j] = a2[j]; }
   }
   __syncthreads();
-  // per group: combine channels (each channel over R thread rows) in double
   const int cpg = C / groups;
   const double n_c = (double)(p1 - p0);
   for (int g = tid; g < groups; g += GN_THREADS) {
@@ -82,110 +116,140 @@ gn_partial_kernel(const u16* __restrict__ x1, const u16* __restrict__ x2, int C1
     GnPart o; o.n = n; o.mean = mean; o.m2 = m2; o.pad = 0;
     part[((long)s * nsplit + split) * groups + g] = o;
   }
-}
-
-__global__ void gn_finalize_kernel(const GnPart* __restrict__ part, int nsplit, int groups, int C, float eps,
-                                   const float* __restrict__ gamma, const float* __restrict__ beta,
-                                   float* __restrict__ scale, float* __restrict__ shift) {
-  __shared__ float mean_s[64], rstd_s[64];
-  const int s = blockIdx.x;
-  for (int g = threadIdx.x; g < groups; g += blockDim.x) {
-    double n = 0.0, mean = 0.0, m2 = 0.0;
-    for (int i = 0; i < nsplit; ++i) {
-      const GnPart p = part[((long)s * nsplit + i) * groups + g];
-      if (p.n <= 0) continue;
-      const double nt = n + p.n;
-      const double d = p.mean - mean;
-      mean += d * p.n / nt;
-      m2 += p.m2 + d * d * n * p.n / nt;
-      n = nt;
+  // ---- publish this block's partials, take an arrival ticket
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(counters + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    is_last = (t == (unsigned)(nsplit - 1));
+  }
+  __syncthreads();
+  if (!is_last) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    counters[s] = 0;  // re-arm for the next call (every block of this sample has arrived)
+  }
+  __syncthreads();
+  // ---- merge the splits: L lanes per group, Chan merge, shuffle tree
+  const int L = GN_THREADS / 64 >= 1 ? (GN_THREADS / (groups > 32 ? 64 : 32)) : 1;  // 8 (G<=32) or 4
+  const int g = tid / L, j = tid % L;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  if (g < groups) {
+    for (int i = j; i < nsplit; i += L) {
+      const GnPart pp = part[((long)s * nsplit + i) * groups + g];
+      chan_merge(n, mean, m2, pp.n, pp.mean, pp.m2);
     }
+  }
+  for (int off = 1; off < L; off <<= 1) {
+    const double nb = shfl_xor_d(n, off), mb = shfl_xor_d(mean, off), qb = shfl_xor_d(m2, off);
+    chan_merge(n, mean, m2, nb, mb, qb);
+  }
+  if (g < groups && j == 0) {
     const double var = n > 0 ? m2 / n : 0.0;
     mean_s[g] = (float)mean;
     rstd_s[g] = (float)(1.0 / sqrt(var + (double)eps));
   }
   __syncthreads();
-  const int cpg = C / groups;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const int g = c / cpg;
-    const float sc = (gamma ? gamma[c] : 1.f) * rstd_s[g];
+  for (int c = tid; c < C; c += GN_THREADS) {
+    const int gg = c / cpg;
+    const float sc = (gamma ? gamma[c] : 1.f) * rstd_s[gg];
     scale[(long)s * C + c] = sc;
-    shift[(long)s * C + c] = (beta ? beta[c] : 0.f) - mean_s[g] * sc;
+    shift[(long)s * C + c] = (beta ? beta[c] : 0.f) - mean_s[gg] * sc;
   }
 }
 
-static int gn_nsplit(int n_samples, long pps) {
-  int ns = cdiv(512, n_samples);
-  ns = (int)std::min<long>(ns, std::max<long>(1, pps / 16));
-  return std::max(1, std::min(ns, 256));
+static int gn_nsplit(int n_samples, long pps, int C) {
+  const long elems = pps * C;
+  long ns = elems / 16384;                       // >= 16K elements (32 KB) per block
+  ns = std::min<long>(ns, cdiv(1024, n_samples));  // ~1024 blocks in total at most
+  ns = std::min<long>(ns, pps);
+  return (int)std::max<long>(1, std::min<long>(ns, 512));
 }
 
-__global__ void affine_act_kernel(const u16* __restrict__ x, long n_chunks, int C, long pps,
-                                  const float* __restrict__ scale, const float* __restrict__ shift, int silu_on,
-                                  u16* __restrict__ y) {
-  const int CC = C / 8;
+// Materialised GroupNorm apply (+SiLU) over an optional channel concat.
+__global__ void gn_apply_kernel(const u16* __restrict__ x1, const u16* __restrict__ x2, int C1, int C2, long n_chunks,
+                                long pps, const float* __restrict__ scale, const float* __restrict__ shift, int silu_on,
+                                u16* __restrict__ y) {
+  const int C = C1 + C2, CC = C / 8;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n_chunks; i += (long)gridDim.x * blockDim.x) {
     const long pix = i / CC;
     const int c = (int)(i - pix * CC) * 8;
     const long s = pix / pps;
+    const uint4 u = c < C1 ? *(const uint4*)(x1 + pix * C1 + c) : *(const uint4*)(x2 + pix * C2 + (c - C1));
+    const float4 s0 = *(const float4*)(scale + s * C + c), s1 = *(const float4*)(scale + s * C + c + 4);
+    const float4 h0 = *(const float4*)(shift + s * C + c), h1 = *(const float4*)(shift + s * C + c + 4);
+    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
     float f[8];
-    unpack8(*(const uint4*)(x + pix * C + c), f);
+    unpack8(u, f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float t = f[j] * scale[s * C + c + j] + shift[s * C + c + j];
+      const float t = f[j] * sc[j] + sh[j];
       f[j] = silu_on ? silu(t) : t;
     }
     *(uint4*)(y + pix * C + c) = pack8(f);
   }
 }
 
-// LayerNorm: one wave per row, row cached in registers (C <= 2048), two-pass.
-constexpr int LN_MAXCH = 4;  // 16-B chunks per lane -> C <= 64*8*4 = 2048
-
+// LayerNorm: 16 lanes per row (4 rows per wave, 16 per block), row cached in
+// registers, two-pass mean / variance, 16-lane shuffle reductions.
+template <int NCH>
 __global__ void __launch_bounds__(256)
 layernorm_kernel(const u16* __restrict__ x, long rows, int C, float eps, const float* __restrict__ gamma,
                  const float* __restrict__ beta, const float* __restrict__ pe, int pe_rpf, int pe_frames,
                  u16* __restrict__ y) {
-  const int lane = threadIdx.x & 63;
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
+  const int sub = threadIdx.x & 15;
+  const long row = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const bool live = row < rows;
   const int CC = C / 8;
-  const u16* xr = x + row * C;
-  float v[LN_MAXCH][8];
+  const u16* xr = x + (live ? row : 0) * C;
+  float v[NCH][8];
   float s = 0.f;
 #pragma unroll
-  for (int q = 0; q < LN_MAXCH; ++q) {
-    const int cc = lane + 64 * q;
+  for (int q = 0; q < NCH; ++q) {
+    const int cc = sub + 16 * q;
     if (cc < CC) {
       unpack8(*(const uint4*)(xr + cc * 8), v[q]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) s += v[q][j];
     }
   }
-  const float mean = wave_sum(s) / C;
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 16);
+  const float mean = s / C;
   float s2 = 0.f;
 #pragma unroll
-  for (int q = 0; q < LN_MAXCH; ++q) {
-    const int cc = lane + 64 * q;
+  for (int q = 0; q < NCH; ++q) {
+    const int cc = sub + 16 * q;
     if (cc < CC) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) { const float d = v[q][j] - mean; s2 += d * d; }
     }
   }
-  const float rstd = rsqrtf(wave_sum(s2) / C + eps);
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, 16);
+  const float rstd = rsqrtf(s2 / C + eps);
+  if (!live) return;
   const float* per = pe ? pe + (long)((row / pe_rpf) % pe_frames) * C : nullptr;
 #pragma unroll
-  for (int q = 0; q < LN_MAXCH; ++q) {
-    const int cc = lane + 64 * q;
+  for (int q = 0; q < NCH; ++q) {
+    const int cc = sub + 16 * q;
     if (cc < CC) {
-      float o[8];
+      const int c = cc * 8;
+      float g[8], b[8], o[8];
+      const float4 g0 = *(const float4*)(gamma + c), g1 = *(const float4*)(gamma + c + 4);
+      const float4 b0 = *(const float4*)(beta + c), b1 = *(const float4*)(beta + c + 4);
+      g[0] = g0.x; g[1] = g0.y; g[2] = g0.z; g[3] = g0.w; g[4] = g1.x; g[5] = g1.y; g[6] = g1.z; g[7] = g1.w;
+      b[0] = b0.x; b[1] = b0.y; b[2] = b0.z; b[3] = b0.w; b[4] = b1.x; b[5] = b1.y; b[6] = b1.z; b[7] = b1.w;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int c = cc * 8 + j;
-        o[j] = (v[q][j] - mean) * rstd * gamma[c] + beta[c];
-        if (per) o[j] += per[c];
+        o[j] = (v[q][j] - mean) * rstd * g[j] + b[j];
+        if (per) o[j] += per[c + j];
       }
-      *(uint4*)(y + row * C + cc * 8) = pack8(o);
+      *(uint4*)(y + row * C + c) = pack8(o);
     }
   }
 }
@@ -195,7 +259,7 @@ layernorm_kernel(const u16* __restrict__ x, long rows, int C, float eps, const f
 using namespace ls;
 
 extern "C" size_t ls_groupnorm_workspace_bytes(int32_t n_samples, int32_t groups) {
-  return (size_t)n_samples * 256 * groups * sizeof(GnPart);
+  return GN_COUNTER_BYTES + (size_t)n_samples * 512 * groups * sizeof(GnPart);
 }
 
 extern "C" int ls_groupnorm(const uint16_t* x1, const uint16_t* x2, int32_t C1, int32_t C2, int32_t n_samples,
@@ -206,36 +270,54 @@ extern "C" int ls_groupnorm(const uint16_t* x1, const uint16_t* x2, int32_t C1, 
     return fail(LS_ERR_INVALID, "ls_groupnorm: bad arguments");
   if (C1 % 8 || C2 % 8 || C % groups || groups > 64 || (C2 && !x2))
     return fail(LS_ERR_INVALID, "ls_groupnorm: channels must be multiples of 8 and groups <= 64");
-  const int ns = gn_nsplit(n_samples, pps);
-  const size_t need = (size_t)n_samples * ns * groups * sizeof(GnPart);
+  if (n_samples > (int)(GN_COUNTER_BYTES / sizeof(unsigned)))
+    return fail(LS_ERR_INVALID, "ls_groupnorm: too many samples");
+  const int ns = gn_nsplit(n_samples, pps, C);
+  const size_t need = GN_COUNTER_BYTES + (size_t)n_samples * ns * groups * sizeof(GnPart);
   if (!workspace || workspace_bytes < need) return fail(LS_ERR_WORKSPACE, "ls_groupnorm: workspace too small");
   const int CC = C / 8;
   const int R = CC <= GN_THREADS ? GN_THREADS / CC : 1;
   const size_t shm = (2 * (size_t)R * C + C) * sizeof(float);
-  if (shm > 64 * 1024) return fail(LS_ERR_INVALID, "ls_groupnorm: too many channels");
-  hipStream_t s = (hipStream_t)stream;
-  gn_partial_kernel<<<dim3(ns, n_samples), GN_THREADS, shm, s>>>(x1, x2, C1, C2, pps, ns, groups, (GnPart*)workspace);
-  int rc = check_launch("gn_partial_kernel");
-  if (rc) return rc;
-  gn_finalize_kernel<<<n_samples, 256, 0, s>>>((const GnPart*)workspace, ns, groups, C, eps, gamma, beta, scale, shift);
-  return check_launch("gn_finalize_kernel");
+  if (shm > 60 * 1024) return fail(LS_ERR_INVALID, "ls_groupnorm: too many channels");
+  unsigned* counters = (unsigned*)workspace;  // zero-initialised by the caller once; re-armed by each call
+  GnPart* part = (GnPart*)((char*)workspace + GN_COUNTER_BYTES);
+  gn_stats_kernel<<<dim3(ns, n_samples), GN_THREADS, shm, (hipStream_t)stream>>>(
+      x1, x2, C1, C2, pps, ns, groups, eps, gamma, beta, part, counters, scale, shift);
+  return check_launch("gn_stats_kernel");
 }
 
-extern "C" int ls_affine_act(const uint16_t* x, int64_t n_pix, int32_t C, int64_t pps, const float* scale,
-                             const float* shift, int32_t silu_on, uint16_t* y, void* stream) {
-  if (!x || !y || C % 8 || n_pix <= 0) return fail(LS_ERR_INVALID, "ls_affine_act: bad arguments");
-  const long n = n_pix * (C / 8);
-  affine_act_kernel<<<(int)std::min<long>(cdiv(n, 256), 8192), 256, 0, (hipStream_t)stream>>>(x, n, C, pps, scale, shift,
-                                                                                             silu_on, y);
-  return check_launch("affine_act_kernel");
+extern "C" int ls_groupnorm_apply(const uint16_t* x1, const uint16_t* x2, int32_t C1, int32_t C2, int64_t n_pix,
+                                  int64_t pps, const float* scale, const float* shift, int32_t silu_on, uint16_t* y,
+                                  void* stream) {
+  if (!x1 || !y || !scale || !shift || (C1 + C2) % 8 || C1 % 8 || n_pix <= 0 || pps <= 0 || (C2 && !x2))
+    return fail(LS_ERR_INVALID, "ls_groupnorm_apply: bad arguments");
+  const long n = n_pix * ((C1 + C2) / 8);
+  gn_apply_kernel<<<(int)std::min<long>(cdiv(n, 256), 16384), 256, 0, (hipStream_t)stream>>>(
+      x1, x2, C1, C2, n, pps, scale, shift, silu_on, y);
+  return check_launch("gn_apply_kernel");
+}
+
+template <int NCH>
+static void launch_ln(const uint16_t* x, int64_t rows, int32_t C, float eps, const float* gamma, const float* beta,
+                      const float* pe, int32_t pe_rpf, int32_t pe_frames, uint16_t* y, hipStream_t s) {
+  layernorm_kernel<NCH><<<cdiv(rows, 16), 256, 0, s>>>(x, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y);
 }
 
 extern "C" int ls_layernorm(const uint16_t* x, int64_t rows, int32_t C, float eps, const float* gamma,
                             const float* beta, const float* pe, int32_t pe_rpf, int32_t pe_frames, uint16_t* y,
                             void* stream) {
-  if (!x || !y || !gamma || !beta || C % 8 || C > 64 * 8 * LN_MAXCH || rows <= 0)
+  if (!x || !y || !gamma || !beta || C % 8 || C > 16 * 8 * 16 || rows <= 0)
     return fail(LS_ERR_INVALID, "ls_layernorm: bad arguments (C % 8 == 0, C <= 2048)");
   if (pe && (pe_rpf <= 0 || pe_frames <= 0)) return fail(LS_ERR_INVALID, "ls_layernorm: bad pe geometry");
-  layernorm_kernel<<<cdiv(rows, 4), 256, 0, (hipStream_t)stream>>>(x, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y);
+  hipStream_t s = (hipStream_t)stream;
+  const int nch = cdiv(C / 8, 16);
+  if (nch <= 1) launch_ln<1>(x, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
+  else if (nch <= 2) launch_ln<2>(x, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
+  else if (nch <= 3) launch_ln<3>(x, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
+  else if (nch <= 5) launch_ln<5>(x, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
+  else if (nch <= 8) launch_ln<8>(x, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
+  else if (nch <= 10) launch_ln<10>(x, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
+  else if (nch <= 12) launch_ln<12>(x, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
+  else launch_ln<16>(x, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
   return check_launch("layernorm_kernel");
 }

@@ -30,7 +30,7 @@ class Workspace:
 
     def __init__(self, device, gemm_bytes=256 << 20, gn_bytes=16 << 20):
         self.gemm = torch.empty(gemm_bytes, dtype=torch.uint8, device=device)
-        self.gn = torch.empty(gn_bytes, dtype=torch.uint8, device=device)
+        self.gn = torch.zeros(gn_bytes, dtype=torch.uint8, device=device)  # GN arrival counters start at 0
 
 
 _WS = {}
@@ -119,14 +119,20 @@ def group_norm(x, groups, eps, gamma, beta, n_samples, x2=None):
     return scale, shift
 
 
-def affine_act(x, scale, shift, n_samples, silu):
+def group_norm_apply(x, scale, shift, n_samples, silu, x2=None):
+    """Materialise act(GN(x | x2)) -> (n, H, W, C1 + C2) bf16."""
     lib = _lib.load()
-    C_ = x.shape[-1]
-    n_pix = x.numel() // C_
-    y = torch.empty_like(x)
-    check(lib.ls_affine_act(_p(x), n_pix, C_, n_pix // n_samples, _p(scale), _p(shift), int(silu), _p(y), _stream()),
-          "ls_affine_act")
+    C1 = x.shape[-1]
+    C2 = x2.shape[-1] if x2 is not None else 0
+    n_pix = x.numel() // C1
+    y = torch.empty(x.shape[:-1] + (C1 + C2,), dtype=torch.bfloat16, device=x.device)
+    check(lib.ls_groupnorm_apply(_p(x), _p(x2), C1, C2, n_pix, n_pix // n_samples, _p(scale), _p(shift), int(silu),
+                                 _p(y), _stream()), "ls_groupnorm_apply")
     return y
+
+
+def affine_act(x, scale, shift, n_samples, silu):
+    return group_norm_apply(x, scale, shift, n_samples, silu)
 
 
 def layer_norm(x2d, gamma, beta, eps=1e-5, pe=None, pe_rows_per_frame=1, pe_frames=1):

@@ -116,11 +116,12 @@ class _Resnet:
         F = n // B
         pps = F * x.shape[1] * x.shape[2]
         s1 = ops.group_norm(x, self.groups, self.eps, *self.n1, B, x2=x2)
-        h = ops.conv(x, self.c1, x2=x2, aff=(s1[0], s1[1], F, True),
-                     rowvec=(temb_all[:, self.temb_slot:], pps, temb_all.shape[1]))
+        a1 = ops.group_norm_apply(x, s1[0], s1[1], B, True, x2=x2)
+        h = ops.conv(a1, self.c1, rowvec=(temb_all[:, self.temb_slot:], pps, temb_all.shape[1]))
         s2 = ops.group_norm(h, self.groups, self.eps, *self.n2, B)
+        a2 = ops.group_norm_apply(h, s2[0], s2[1], B, True)
         res = x if self.sc is None else ops.conv(x, self.sc, x2=x2)
-        return ops.conv(h, self.c2, aff=(s2[0], s2[1], F, True), res=res, out_scale=self.out_scale)
+        return ops.conv(a2, self.c2, res=res, out_scale=self.out_scale)
 
 
 class _Transformer:
@@ -353,8 +354,7 @@ class _DeviceUNet:
             if us is not None:
                 h = ops.conv(h, us, upsample=True)
         sc = ops.group_norm(h, self.groups, self.eps, *self.norm_out, B)
-        F = h.shape[0] // B
-        return ops.conv(h, self.conv_out, aff=(sc[0], sc[1], F, True))
+        return ops.conv(ops.group_norm_apply(h, sc[0], sc[1], B, True), self.conv_out)
 
 
 # --------------------------------------------------------------------------

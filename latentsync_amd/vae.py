@@ -47,10 +47,10 @@ class _Res:
     def __call__(self, x):
         n = x.shape[0]
         s1 = ops.group_norm(x, 32, 1e-6, *self.n1, n)
-        h = ops.conv(x, self.c1, aff=(s1[0], s1[1], 1, True))
+        h = ops.conv(ops.group_norm_apply(x, s1[0], s1[1], n, True), self.c1)
         s2 = ops.group_norm(h, 32, 1e-6, *self.n2, n)
         res = x if self.sc is None else ops.conv(x, self.sc)
-        return ops.conv(h, self.c2, aff=(s2[0], s2[1], 1, True), res=res)
+        return ops.conv(ops.group_norm_apply(h, s2[0], s2[1], n, True), self.c2, res=res)
 
 
 class _Attn:
@@ -114,7 +114,7 @@ class _DeviceVAE:
         for blk in self.enc_mid:
             h = blk(h)
         s = ops.group_norm(h, 32, 1e-6, *self.enc_norm, h.shape[0])
-        h = ops.conv(h, self.enc_out, aff=(s[0], s[1], 1, True))
+        h = ops.conv(ops.group_norm_apply(h, s[0], s[1], h.shape[0], True), self.enc_out)
         return ops.conv(h, self.quant, out_f32=True)
 
     def decode(self, z):
@@ -129,7 +129,7 @@ class _DeviceVAE:
             if us is not None:
                 h = ops.conv(h, us, upsample=True)
         s = ops.group_norm(h, 32, 1e-6, *self.dec_norm, h.shape[0])
-        return ops.conv(h, self.dec_out, aff=(s[0], s[1], 1, True))
+        return ops.conv(ops.group_norm_apply(h, s[0], s[1], h.shape[0], True), self.dec_out)
 
 
 class DiagonalGaussianDistribution:
