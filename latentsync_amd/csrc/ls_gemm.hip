@@ -152,6 +152,73 @@ __device__ __forceinline__ uint4 load_a_chunk(const ConvArgs& a, int kt, int ch,
 
 __device__ __forceinline__ int swz(int row, int ch) { return row * 8 + (ch ^ ((row >> 1) & 7)); }
 
+// Stage the accumulator tile through LDS one wave-row (WTM rows) at a time, then
+// each thread handles whole 8-column chunks (split-K slab / GEGLU / plain).
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void store_tile(const ConvArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16], float* st,
+                                           int m0, int n0, int z) {
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  constexpr int SP = BN + 4;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const bool vec = (a.N % 8 == 0) && (a.ldy % 8 == 0) && (!a.res || a.ldr % 8 == 0);
+  const bool geglu = a.act == LS_ACT_GEGLU;
+#pragma unroll 1
+  for (int p = 0; p < WM; ++p) {
+    if (wm == p) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            st[(i * 16 + (lane >> 4) * 4 + r) * SP + wn * WTN + j * 16 + (lane & 15)] = acc[i][j][r];
+    }
+    __syncthreads();
+    const int rbase = m0 + p * WTM;
+    if (a.split > 1) {
+      float* P = a.partial + (long)z * a.M * a.N;
+      for (int q = tid; q < WTM * (BN / 8); q += 256) {
+        const int r = q / (BN / 8), c8 = (q - r * (BN / 8)) * 8;
+        const int row = rbase + r, col = n0 + c8;
+        if (row >= a.M || col >= a.N) continue;
+        const float* s = st + r * SP + c8;
+        if (vec) {
+          *(float4*)(P + (long)row * a.N + col) = *(const float4*)s;
+          *(float4*)(P + (long)row * a.N + col + 4) = *(const float4*)(s + 4);
+        } else {
+          for (int j = 0; j < 8 && col + j < a.N; ++j) P[(long)row * a.N + col + j] = s[j];
+        }
+      }
+    } else if (geglu) {
+      for (int q = tid; q < WTM * (BN / 16); q += 256) {
+        const int r = q / (BN / 16), o8 = (q - r * (BN / 16)) * 8;
+        const int ph = (o8 >> 4) * 32 + (o8 & 15);
+        const int row = rbase + r, col = n0 + ph;
+        if (col >= a.N) continue;
+        float h[8], g[8];
+        const float* s = st + r * SP + ph;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { h[j] = s[j]; g[j] = s[16 + j]; }
+        epi_geglu8(a, row, col, h, g, vec);
+      }
+    } else {
+      for (int q = tid; q < WTM * (BN / 8); q += 256) {
+        const int r = q / (BN / 8), c8 = (q - r * (BN / 8)) * 8;
+        const int row = rbase + r, col = n0 + c8;
+        if (col >= a.N) continue;
+        float v[8];
+        const float* s = st + r * SP + c8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = s[j];
+        epi_chunk(a, row, col, v, vec && col + 8 <= a.N);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <int BM, int BN, int WM, int WN, int KS, bool TAPU>
 __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvArgs a) {
   constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -244,65 +311,153 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvArgs a) {
     }
   }
 
-  // ---------------------------------------------------------------- epilogue
-  // Stage the tile through LDS one wave-row (WTM rows) at a time, then each
-  // thread handles whole 8-column chunks.
-  float* st = (float*)&lds[0][0];
-  const bool vec = (a.N % 8 == 0) && (a.ldy % 8 == 0) && (!a.res || a.ldr % 8 == 0);
-  const bool geglu = a.act == LS_ACT_GEGLU;
-#pragma unroll 1
-  for (int p = 0; p < WM; ++p) {
-    if (wm == p) {
+  store_tile<BM, BN, WM, WN>(a, acc, (float*)&lds[0][0], m0, n0, z);
+}
+
+
+// ------------------------------------------------------------------ DMA path
+// Same tiles / LDS image / epilogue, but both operands stream global -> LDS with
+// global_load_lds_dwordx4 (no VGPR staging, no ds_write).  The LDS image is
+// written lane-linearly, so the XOR swizzle is applied on the per-lane SOURCE
+// address (logical chunk = physical chunk ^ ((row >> 1) & 7)).  Out-of-range /
+// padding taps read a zero page.  Two LDS buffers: tile k+1's DMA overlaps tile
+// k's MFMAs; counted vmcnt + raw s_barrier so the in-flight tile is not drained.
+__device__ uint4 ls_zero_page[2];
+
+__device__ __forceinline__ void glds16(const void* src, uint4* lds_dst) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+
+template <int KS, bool TAPU>
+__device__ __forceinline__ const void* a_src(const ConvArgs& a, int kt, int c, int m, const RowGeo& g) {
+  const void* zero = (const void*)ls_zero_page;
+  int cg, tap = 0;
+  if (KS == 1) {
+    cg = kt * 64 + c * 8;
+    if (m >= a.M || cg >= a.Cin) return zero;
+  } else if (TAPU) {
+    tap = (kt * 64) / a.Cin;
+    cg = kt * 64 - tap * a.Cin + c * 8;
+  } else {
+    const int kc = kt * 8 + c;
+    tap = kc / a.CC;
+    cg = (kc - tap * a.CC) * 8;
+    if (tap >= 9) return zero;
+  }
+  long pix;
+  if (KS == 1) {
+    pix = m;
+  } else {
+    const int kh = tap / 3, kw = tap - kh * 3;
+    int yy = g.yb + kh, xx = g.xb + kw;
+    if (a.upsample) {
+      if ((unsigned)yy >= (unsigned)(2 * a.H) || (unsigned)xx >= (unsigned)(2 * a.W)) return zero;
+      yy >>= 1; xx >>= 1;
+    } else {
+      if ((unsigned)yy >= (unsigned)a.H || (unsigned)xx >= (unsigned)a.W) return zero;
+    }
+    pix = (long)g.pb + yy * a.W + xx;
+  }
+  if (cg < a.C1) return a.x1 + pix * a.ld1 + cg;
+  return a.x2 + pix * a.ld2 + (cg - a.C1);
+}
+
+template <int BM, int BN, int WM, int WN, int KS, bool TAPU>
+__global__ void __launch_bounds__(256) conv_gemm_dma_kernel(ConvArgs a) {
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  constexpr int AI = BM / 32, BI = BN / 32;  // DMA wave-instructions per wave per K-tile
+  __shared__ uint4 lds[2][(BM + BN) * 8];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  int bid = blockIdx.x;
+  const int nt = a.ntm * a.ntn;
+  const int z = bid / nt;
+  bid -= z * nt;
+  const int tm = bid / a.ntn, tn = bid - tm * a.ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kt0 = z * a.kt_per_split;
+  const int kt1 = min(a.ktiles, kt0 + a.kt_per_split);
+
+  // lane -> (row, logical chunk) of each DMA instruction
+  int arow[AI], ach[AI], brow[BI], bch[BI];
+  RowGeo geo[AI];
+#pragma unroll
+  for (int p = 0; p < AI; ++p) {
+    const int q = (wid * AI + p) * 64 + lane;
+    const int row = q >> 3;
+    arow[p] = m0 + row;
+    ach[p] = (q & 7) ^ ((row >> 1) & 7);
+    if (KS == 3) {
+      const int m = m0 + row;
+      const int hw = a.Ho * a.Wo;
+      const int n = m / hw, r = m - n * hw;
+      const int yo = r / a.Wo, xo = r - yo * a.Wo;
+      geo[p].pb = n * a.H * a.W;
+      geo[p].yb = (m < a.M) ? (a.upsample ? yo - a.pad : yo * a.stride - a.pad) : -(1 << 28);
+      geo[p].xb = a.upsample ? xo - a.pad : xo * a.stride - a.pad;
+    } else {
+      geo[p].pb = 0; geo[p].yb = 0; geo[p].xb = 0;
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < BI; ++p) {
+    const int q = (wid * BI + p) * 64 + lane;
+    const int row = q >> 3;
+    brow[p] = n0 + row;
+    bch[p] = (q & 7) ^ ((row >> 1) & 7);
+  }
+  auto issue = [&](int kt, int buf) {
+#pragma unroll
+    for (int p = 0; p < AI; ++p)
+      glds16(a_src<KS, TAPU>(a, kt, ach[p], arow[p], geo[p]), &lds[buf][(wid * AI + p) * 64]);
+#pragma unroll
+    for (int p = 0; p < BI; ++p) {
+      const void* src = brow[p] < a.N ? (const void*)(a.w + (long)brow[p] * a.K + kt * 64 + bch[p] * 8)
+                                      : (const void*)ls_zero_page;
+      glds16(src, &lds[buf][BM * 8 + (wid * BI + p) * 64]);
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  if (kt0 < kt1) issue(kt0, 0);
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int cur = (kt - kt0) & 1;
+    if (kt + 1 < kt1) {
+      issue(kt + 1, cur ^ 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(AI + BI) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = ks * 4 + (lane >> 4);
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        af[i] = __builtin_bit_cast(bf16x8, lds[cur][swz(wm * WTM + i * 16 + (lane & 15), c)]);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bfr[j] = __builtin_bit_cast(bf16x8, lds[cur][BM * 8 + swz(wn * WTN + j * 16 + (lane & 15), c)]);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            st[(i * 16 + (lane >> 4) * 4 + r) * SP + wn * WTN + j * 16 + (lane & 15)] = acc[i][j][r];
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    __syncthreads();
-    const int rbase = m0 + p * WTM;
-    if (a.split > 1) {
-      float* P = a.partial + (long)z * a.M * a.N;
-      for (int q = tid; q < WTM * (BN / 8); q += 256) {
-        const int r = q / (BN / 8), c8 = (q - r * (BN / 8)) * 8;
-        const int row = rbase + r, col = n0 + c8;
-        if (row >= a.M || col >= a.N) continue;
-        const float* s = st + r * SP + c8;
-        if (vec) {
-          *(float4*)(P + (long)row * a.N + col) = *(const float4*)s;
-          *(float4*)(P + (long)row * a.N + col + 4) = *(const float4*)(s + 4);
-        } else {
-          for (int j = 0; j < 8 && col + j < a.N; ++j) P[(long)row * a.N + col + j] = s[j];
-        }
-      }
-    } else if (geglu) {
-      for (int q = tid; q < WTM * (BN / 16); q += 256) {
-        const int r = q / (BN / 16), o8 = (q - r * (BN / 16)) * 8;
-        const int ph = (o8 >> 4) * 32 + (o8 & 15);
-        const int row = rbase + r, col = n0 + ph;
-        if (col >= a.N) continue;
-        float h[8], g[8];
-        const float* s = st + r * SP + ph;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) { h[j] = s[j]; g[j] = s[16 + j]; }
-        epi_geglu8(a, row, col, h, g, vec);
-      }
-    } else {
-      for (int q = tid; q < WTM * (BN / 8); q += 256) {
-        const int r = q / (BN / 8), c8 = (q - r * (BN / 8)) * 8;
-        const int row = rbase + r, col = n0 + c8;
-        if (col >= a.N) continue;
-        float v[8];
-        const float* s = st + r * SP + c8;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = s[j];
-        epi_chunk(a, row, col, v, vec && col + 8 <= a.N);
-      }
-    }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
   }
+  store_tile<BM, BN, WM, WN>(a, acc, (float*)&lds[0][0], m0, n0, z);
 }
 
 // split-K reduction + epilogue: one thread per 8 output columns
@@ -344,6 +499,8 @@ __global__ void splitk_reduce_kernel(ConvArgs a) {
 }
 
 // ---------------------------------------------------------------- host side
+static bool g_force_regstage = getenv("LS_GEMM_REGSTAGE") != nullptr;
+
 struct TileCfg { int bm, bn, split; };
 
 // Tile + split-K choice by a small cost model: time ~ max(1, blocks / CUs) x
@@ -371,9 +528,15 @@ static TileCfg pick_tile(long M, int N, int ktiles, bool allow_split) {
 
 template <int BM, int BN, int WM, int WN>
 static void launch_cfg(const ConvArgs& a, int ks, bool tapu, int grid, hipStream_t s) {
-  if (ks == 1) conv_gemm_kernel<BM, BN, WM, WN, 1, false><<<grid, 256, 0, s>>>(a);
-  else if (tapu) conv_gemm_kernel<BM, BN, WM, WN, 3, true><<<grid, 256, 0, s>>>(a);
-  else conv_gemm_kernel<BM, BN, WM, WN, 3, false><<<grid, 256, 0, s>>>(a);
+  if (a.aff_scale || g_force_regstage) {  // prologue needs the register path
+    if (ks == 1) conv_gemm_kernel<BM, BN, WM, WN, 1, false><<<grid, 256, 0, s>>>(a);
+    else if (tapu) conv_gemm_kernel<BM, BN, WM, WN, 3, true><<<grid, 256, 0, s>>>(a);
+    else conv_gemm_kernel<BM, BN, WM, WN, 3, false><<<grid, 256, 0, s>>>(a);
+  } else {
+    if (ks == 1) conv_gemm_dma_kernel<BM, BN, WM, WN, 1, false><<<grid, 256, 0, s>>>(a);
+    else if (tapu) conv_gemm_dma_kernel<BM, BN, WM, WN, 3, true><<<grid, 256, 0, s>>>(a);
+    else conv_gemm_dma_kernel<BM, BN, WM, WN, 3, false><<<grid, 256, 0, s>>>(a);
+  }
 }
 
 static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split) {

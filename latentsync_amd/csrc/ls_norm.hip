@@ -21,8 +21,9 @@ __device__ __forceinline__ void chan_merge(double& n, double& mean, double& m2, 
   if (nb <= 0) return;
   const double nt = n + nb;
   const double d = meanb - mean;
-  mean += d * nb / nt;
-  m2 += m2b + d * d * n * nb / nt;
+  const double f = nb / nt;  // one fp64 division per merge
+  mean += d * f;
+  m2 += m2b + d * d * n * f;
   n = nt;
 }
 
@@ -134,7 +135,7 @@ gn_stats_kernel(const u16* __restrict__ x1, const u16* __restrict__ x2, int C1, 
   }
   __syncthreads();
   // ---- merge the splits: L lanes per group, Chan merge, shuffle tree
-  const int L = GN_THREADS / 64 >= 1 ? (GN_THREADS / (groups > 32 ? 64 : 32)) : 1;  // 8 (G<=32) or 4
+  const int L = groups > 32 ? 4 : 8;  // lanes per group (power of two, inside one wave)
   const int g = tid / L, j = tid % L;
   double n = 0.0, mean = 0.0, m2 = 0.0;
   if (g < groups) {
@@ -163,10 +164,10 @@ gn_stats_kernel(const u16* __restrict__ x1, const u16* __restrict__ x2, int C1, 
 
 static int gn_nsplit(int n_samples, long pps, int C) {
   const long elems = pps * C;
-  long ns = elems / 16384;                       // >= 16K elements (32 KB) per block
-  ns = std::min<long>(ns, cdiv(1024, n_samples));  // ~1024 blocks in total at most
-  ns = std::min<long>(ns, pps);
-  return (int)std::max<long>(1, std::min<long>(ns, 512));
+  long ns = elems / 65536;                        // >= 64K elements (128 KB) per block
+  ns = std::min<long>(ns, cdiv(512, n_samples));  // <= ~512 blocks in total
+  ns = std::min<long>(ns, pps / 8);
+  return (int)std::max<long>(1, std::min<long>(ns, 256));
 }
 
 // Materialised GroupNorm apply (+SiLU) over an optional channel concat.

@@ -52,7 +52,7 @@ class WindowEngine:
     """Device-resident executor of one 16-frame window; see module docstring."""
 
     def __init__(self, unet, vae, scheduler, num_frames=16, resolution=256, num_inference_steps=20,
-                 guidance_scale=1.0, use_graphs=True, audio_tokens=50):
+                 guidance_scale=1.0, use_graphs=True, audio_tokens=50, windows=1):
         self.unet, self.vae, self.scheduler = unet, vae, scheduler
         self.ud = unet._require_device()
         self.vd = vae._require()
@@ -62,11 +62,16 @@ class WindowEngine:
         self.steps, self.g = num_inference_steps, float(guidance_scale)
         self.Bu = 2 if guidance_scale > 1.0 else 1
         self.L = audio_tokens
-        self.P = self.F * self.h * self.h
+        # `windows` independent windows are batched through one UNet call (UNet batch
+        # = Bu * windows samples, ordered [uncond w0..wN-1, cond w0..wN-1]); every
+        # per-sample op (5-D GroupNorm, temporal attention) stays per window.
+        self.nw = windows
+        self.FT = self.F * windows  # frames in flight
+        self.P = self.FT * self.h * self.h
         scheduler.set_timesteps(num_inference_steps)
         self.ts = scheduler.timesteps.to(torch.int32).to(dev)
         self.coef = scheduler.coef_table(dev)
-        F_, R, h, Bu, P = self.F, self.R, self.h, self.Bu, self.P
+        F_, R, h, Bu, P = self.FT, self.R, self.h, self.Bu, self.P
         cd = unet.config.cross_attention_dim
         z = lambda *s, dt=torch.bfloat16: torch.zeros(s, dtype=dt, device=dev)
         self.faces = z(F_, 3, R, R, dt=torch.uint8)
@@ -95,11 +100,11 @@ class WindowEngine:
         mom = self.vd.encode_moments(self.pix)
         ops.vae_sample(mom, self.eps_r, SCALING, 0.0, self.cond, 9)
         self.lat.copy_(self.init_lat)
-        ops.pack_unet_input(self.lat, self.cond, self.mask, self.F, self.R, self.h, self.Bu, self.unet_in)
+        ops.pack_unet_input(self.lat, self.cond, self.mask, self.FT, self.R, self.h, self.Bu, self.unet_in)
         self.step.zero_()
 
     def _step(self):
-        eps = self.ud.forward(self.unet_in, self.Bu, self.ts, self.step, self.audio, self.L)
+        eps = self.ud.forward(self.unet_in, self.Bu * self.nw, self.ts, self.step, self.audio, self.L)
         ops.ddim_cfg_step(eps, self.Bu, self.g, self.lat, self.coef, self.step, self.unet_in)
 
     def _decode(self):
@@ -125,10 +130,11 @@ class WindowEngine:
 
     # -- inputs / execution -------------------------------------------------------
     def load(self, faces_u8, mask, audio_chunks, init_latent, eps_masked, eps_ref):
-        """Stage one window's inputs into the static device buffers.
-        faces (F,3,R,R) uint8; mask (R,R) keep-mask; audio (F,50,384);
-        init_latent (1,4,1,h,w) or (1,4,F,h,w); eps_* (F,4,h,w)."""
-        F_, h = self.F, self.h
+        """Stage the inputs of `windows` consecutive windows into the static buffers.
+        faces (W*F,3,R,R) uint8; mask (R,R) keep-mask; audio (W*F,50,384);
+        init_latent (W or 1, 4, 1 or F, h, w) (one draw per window, repeated over its
+        frames as prepare_latents does); eps_* (W*F,4,h,w)."""
+        F_, h = self.FT, self.h
         self.faces.copy_(faces_u8)
         self.mask.copy_(mask)
         a = audio_chunks.reshape(F_ * self.L, -1).to(torch.bfloat16)
@@ -138,9 +144,10 @@ class WindowEngine:
         else:
             self.audio.copy_(a)
         il = init_latent.float()
-        if il.shape[2] == 1:
-            il = il.expand(1, 4, F_, h, h)
-        self.init_lat.copy_(il[0].permute(1, 2, 3, 0).reshape(-1, 4))
+        if il.shape[0] == 1 and self.nw > 1:
+            il = il.expand(self.nw, *il.shape[1:])
+        il = il.expand(self.nw, 4, self.F, h, h)  # (W, 4, F, h, w)
+        self.init_lat.copy_(il.permute(0, 2, 3, 4, 1).reshape(-1, 4))
         self.eps_m.copy_(eps_masked.float().permute(0, 2, 3, 1).reshape(-1, 4))
         self.eps_r.copy_(eps_ref.float().permute(0, 2, 3, 1).reshape(-1, 4))
 
