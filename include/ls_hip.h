@@ -207,6 +207,12 @@ int ls_paste_back(const uint16_t* dec, int32_t ld_dec, const uint16_t* pix, int3
 int ls_add_rows(const uint16_t* x, int64_t rows, int32_t C, int32_t ldx, const float* table, int32_t table_rows,
                 uint16_t* y, int32_t ldy, void* stream);
 
+/* Tuning / A-B switches for ls_conv2d (process-wide, host side only):
+ * key 1 = force the register-staged kernel (1) instead of the LDS-DMA one;
+ * key 2 = force tile 0 auto, 1 128x128, 2 128x64, 3 64x64, 4 128x32; key 3 = split-K with key 2;
+ * key 4 = ablation (1 skip MFMA, 2 skip operand DMA; timing only); key 5 = DMA K-tile depth 32 or 64. */
+int ls_set_tuning(int32_t key, int32_t value);
+
 int ls_abi_version(void);
 const char* ls_last_error(void);
 

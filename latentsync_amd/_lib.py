@@ -69,6 +69,7 @@ _SIGS = {
                                      C.c_int32, c_vp]),
     "ls_scale_latents": (C.c_int, [c_vp, C.c_int64, C.c_float, C.c_float, c_vp, C.c_int32, c_vp]),
     "ls_paste_back": (C.c_int, [c_vp, C.c_int32, c_vp, C.c_int32, c_vp, C.c_int32, C.c_int32, c_vp, c_vp, c_vp]),
+    "ls_set_tuning": (C.c_int, [C.c_int32, C.c_int32]),
     "ls_add_rows": (C.c_int, [c_vp, C.c_int64, C.c_int32, C.c_int32, c_vp, C.c_int32, c_vp, C.c_int32, c_vp]),
 }
 

@@ -27,6 +27,7 @@ struct ConvArgs {
   void* y; int ldy; int y_f32;
   int ktiles, kt_per_split, split; float* partial;
   int ntm, ntn;
+  int ablate;  // tuning only: 1 = skip MFMAs, 2 = skip operand DMA
 };
 
 // ---------------------------------------------------------------- epilogue
@@ -328,67 +329,94 @@ __device__ __forceinline__ void glds16(const void* src, uint4* lds_dst) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
 }
 
-template <int KS, bool TAPU>
+template <int KS, bool TAPU, int BK = 64>
 __device__ __forceinline__ const void* a_src(const ConvArgs& a, int kt, int c, int m, const RowGeo& g) {
-  const void* zero = (const void*)ls_zero_page;
+  // branch-free: compute the candidate address, then select it or the zero page
   int cg, tap = 0;
+  bool ok;
   if (KS == 1) {
-    cg = kt * 64 + c * 8;
-    if (m >= a.M || cg >= a.Cin) return zero;
+    cg = kt * BK + c * 8;
+    ok = (m < a.M) & (cg < a.Cin);
   } else if (TAPU) {
-    tap = (kt * 64) / a.Cin;
-    cg = kt * 64 - tap * a.Cin + c * 8;
+    tap = (kt * BK) / a.Cin;
+    cg = kt * BK - tap * a.Cin + c * 8;
+    ok = true;
   } else {
-    const int kc = kt * 8 + c;
+    const int kc = kt * (BK / 8) + c;
     tap = kc / a.CC;
     cg = (kc - tap * a.CC) * 8;
-    if (tap >= 9) return zero;
+    ok = tap < 9;
   }
-  long pix;
+  int pix;
   if (KS == 1) {
     pix = m;
   } else {
     const int kh = tap / 3, kw = tap - kh * 3;
     int yy = g.yb + kh, xx = g.xb + kw;
-    if (a.upsample) {
-      if ((unsigned)yy >= (unsigned)(2 * a.H) || (unsigned)xx >= (unsigned)(2 * a.W)) return zero;
-      yy >>= 1; xx >>= 1;
-    } else {
-      if ((unsigned)yy >= (unsigned)a.H || (unsigned)xx >= (unsigned)a.W) return zero;
-    }
-    pix = (long)g.pb + yy * a.W + xx;
+    const int lim_y = a.upsample ? 2 * a.H : a.H, lim_x = a.upsample ? 2 * a.W : a.W;
+    ok &= ((unsigned)yy < (unsigned)lim_y) & ((unsigned)xx < (unsigned)lim_x);
+    yy >>= a.upsample;
+    xx >>= a.upsample;
+    pix = g.pb + yy * a.W + xx;
   }
-  if (cg < a.C1) return a.x1 + pix * a.ld1 + cg;
-  return a.x2 + pix * a.ld2 + (cg - a.C1);
+  const bool second = cg >= a.C1;
+  const u16* base = second ? a.x2 : a.x1;
+  const long off = (long)pix * (second ? a.ld2 : a.ld1) + (second ? cg - a.C1 : cg);
+  return ok ? (const void*)(base + off) : (const void*)ls_zero_page;
 }
 
-template <int BM, int BN, int WM, int WN, int KS, bool TAPU>
+// XCD-aware block order: blocks b and b+8 share an XCD under round-robin
+// dispatch, so give every XCD a contiguous range of tiles (shared A rows /
+// 3x3 halos / weight panels stay in one L2).  Bijective for any grid size.
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = b % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+}
+
+template <int N> __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// LDS image of one operand tile: rows of BK bf16, 16-B chunks XOR-swizzled so
+// the 16-lane groups of a ds_read_b128 fragment read hit distinct bank slots.
+template <int BK>
+__device__ __forceinline__ int swz_bk(int row, int c) {
+  if (BK == 64) return row * 8 + (c ^ ((row >> 1) & 7));
+  return row * 4 + (c ^ ((-(row >> 2)) & 3));
+}
+
+template <int BM, int BN, int WM, int WN, int KS, bool TAPU, int NST, int BK>
 __global__ void __launch_bounds__(256) conv_gemm_dma_kernel(ConvArgs a) {
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int FM = WTM / 16, FN = WTN / 16;
-  constexpr int AI = BM / 32, BI = BN / 32;  // DMA wave-instructions per wave per K-tile
-  __shared__ uint4 lds[2][(BM + BN) * 8];
+  constexpr int CPR = BK / 8;                         // 16-B chunks per row
+  constexpr int AI = BM * CPR / 256, BI = BN * CPR / 256;  // DMA wave-instructions per wave per K-tile
+  constexpr int L = AI + BI;
+  constexpr int KSTEPS = BK / 32;
+  constexpr int STAGE = (BM + BN) * CPR;              // uint4 per stage
+  extern __shared__ __attribute__((aligned(16))) uint4 lds_dyn[];
+  uint4* lds = lds_dyn;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  int bid = blockIdx.x;
   const int nt = a.ntm * a.ntn;
+  int bid = xcd_remap(blockIdx.x, nt * a.split);
   const int z = bid / nt;
   bid -= z * nt;
   const int tm = bid / a.ntn, tn = bid - tm * a.ntn;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int kt0 = z * a.kt_per_split;
-  const int kt1 = min(a.ktiles, kt0 + a.kt_per_split);
+  const int ktiles = a.K / BK;
+  const int kps = a.kt_per_split * (64 / BK);
+  const int kt0 = z * kps;
+  const int kt1 = min(ktiles, kt0 + kps);
 
-  // lane -> (row, logical chunk) of each DMA instruction
   int arow[AI], ach[AI], brow[BI], bch[BI];
   RowGeo geo[AI];
 #pragma unroll
   for (int p = 0; p < AI; ++p) {
     const int q = (wid * AI + p) * 64 + lane;
-    const int row = q >> 3;
+    const int row = q / CPR;
+    const int pc = q % CPR;
     arow[p] = m0 + row;
-    ach[p] = (q & 7) ^ ((row >> 1) & 7);
+    ach[p] = swz_bk<BK>(row, pc) - row * CPR;  // logical chunk stored at physical chunk pc (involution)
     if (KS == 3) {
       const int m = m0 + row;
       const int hw = a.Ho * a.Wo;
@@ -404,19 +432,20 @@ __global__ void __launch_bounds__(256) conv_gemm_dma_kernel(ConvArgs a) {
 #pragma unroll
   for (int p = 0; p < BI; ++p) {
     const int q = (wid * BI + p) * 64 + lane;
-    const int row = q >> 3;
+    const int row = q / CPR;
     brow[p] = n0 + row;
-    bch[p] = (q & 7) ^ ((row >> 1) & 7);
+    bch[p] = swz_bk<BK>(row, q % CPR) - row * CPR;
   }
-  auto issue = [&](int kt, int buf) {
+  auto issue = [&](int kt, int stage) {
+    uint4* base = lds + stage * STAGE;
 #pragma unroll
     for (int p = 0; p < AI; ++p)
-      glds16(a_src<KS, TAPU>(a, kt, ach[p], arow[p], geo[p]), &lds[buf][(wid * AI + p) * 64]);
+      glds16(a_src<KS, TAPU, BK>(a, kt, ach[p], arow[p], geo[p]), base + (wid * AI + p) * 64);
 #pragma unroll
     for (int p = 0; p < BI; ++p) {
-      const void* src = brow[p] < a.N ? (const void*)(a.w + (long)brow[p] * a.K + kt * 64 + bch[p] * 8)
+      const void* src = brow[p] < a.N ? (const void*)(a.w + (long)brow[p] * a.K + kt * BK + bch[p] * 8)
                                       : (const void*)ls_zero_page;
-      glds16(src, &lds[buf][BM * 8 + (wid * BI + p) * 64]);
+      glds16(src, base + BM * CPR + (wid * BI + p) * 64);
     }
   };
 
@@ -426,38 +455,45 @@ __global__ void __launch_bounds__(256) conv_gemm_dma_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  if (kt0 < kt1) issue(kt0, 0);
+  const bool do_dma = a.ablate != 2;
+#pragma unroll
+  for (int t = 0; t < NST - 1; ++t)
+    if (kt0 + t < kt1 && do_dma) issue(kt0 + t, t);
+  int stage = 0;
   for (int kt = kt0; kt < kt1; ++kt) {
-    const int cur = (kt - kt0) & 1;
-    if (kt + 1 < kt1) {
-      issue(kt + 1, cur ^ 1);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(AI + BI) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (kt + NST - 1 < kt1 && do_dma) issue(kt + NST - 1, (stage + NST - 1) % NST);
+    const int ahead = min(NST - 1, kt1 - 1 - kt);
+    if (NST >= 4 && ahead >= 3) wait_vm<3 * L>();
+    else if (NST >= 3 && ahead >= 2) wait_vm<2 * L>();
+    else if (ahead >= 1) wait_vm<L>();
+    else wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    const uint4* cur = lds + stage * STAGE;
+    bf16x8 af[KSTEPS][FM], bfr[KSTEPS][FN];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < KSTEPS; ++ks) {
       const int c = ks * 4 + (lane >> 4);
-      bf16x8 af[FM], bfr[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i)
-        af[i] = __builtin_bit_cast(bf16x8, lds[cur][swz(wm * WTM + i * 16 + (lane & 15), c)]);
+        af[ks][i] = __builtin_bit_cast(bf16x8, cur[swz_bk<BK>(wm * WTM + i * 16 + (lane & 15), c)]);
 #pragma unroll
       for (int j = 0; j < FN; ++j)
-        bfr[j] = __builtin_bit_cast(bf16x8, lds[cur][BM * 8 + swz(wn * WTN + j * 16 + (lane & 15), c)]);
+        bfr[ks][j] = __builtin_bit_cast(bf16x8, cur[BM * CPR + swz_bk<BK>(wn * WTN + j * 16 + (lane & 15), c)]);
+    }
+#pragma unroll
+    for (int ks = 0; ks < KSTEPS; ++ks)
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bfr[ks][j], acc[i][j], 0, 0, 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    stage = stage + 1 == NST ? 0 : stage + 1;
   }
-  store_tile<BM, BN, WM, WN>(a, acc, (float*)&lds[0][0], m0, n0, z);
+  store_tile<BM, BN, WM, WN>(a, acc, (float*)lds, m0, n0, z);
 }
 
 // split-K reduction + epilogue: one thread per 8 output columns
@@ -500,6 +536,7 @@ __global__ void splitk_reduce_kernel(ConvArgs a) {
 
 // ---------------------------------------------------------------- host side
 static bool g_force_regstage = getenv("LS_GEMM_REGSTAGE") != nullptr;
+static int g_force_tile = 0, g_force_split = 0, g_ablate = 0, g_bk = 64;
 
 struct TileCfg { int bm, bn, split; };
 
@@ -526,6 +563,27 @@ static TileCfg pick_tile(long M, int N, int ktiles, bool allow_split) {
   return best;
 }
 
+template <int BM, int BN, int WM, int WN, int KS, bool TAPU, int NST, int BK>
+static void launch_dma1(const ConvArgs& a, int grid, hipStream_t s) {
+  // staging for the epilogue must fit too
+  const size_t shm = std::max<size_t>((size_t)NST * (BM + BN) * (BK / 8) * 16, (size_t)(BM / WM) * (BN + 4) * 4);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)conv_gemm_dma_kernel<BM, BN, WM, WN, KS, TAPU, NST, BK>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    attr = true;
+  }
+  conv_gemm_dma_kernel<BM, BN, WM, WN, KS, TAPU, NST, BK><<<grid, 256, shm, s>>>(a);
+}
+
+template <int BM, int BN, int WM, int WN, int KS, bool TAPU>
+static void launch_dma(const ConvArgs& a, int grid, hipStream_t s) {
+  if constexpr (BN >= 64) {
+    if (g_bk == 32) { launch_dma1<BM, BN, WM, WN, KS, TAPU, 3, 32>(a, grid, s); return; }
+  }
+  launch_dma1<BM, BN, WM, WN, KS, TAPU, 2, 64>(a, grid, s);
+}
+
 template <int BM, int BN, int WM, int WN>
 static void launch_cfg(const ConvArgs& a, int ks, bool tapu, int grid, hipStream_t s) {
   if (a.aff_scale || g_force_regstage) {  // prologue needs the register path
@@ -533,9 +591,9 @@ static void launch_cfg(const ConvArgs& a, int ks, bool tapu, int grid, hipStream
     else if (tapu) conv_gemm_kernel<BM, BN, WM, WN, 3, true><<<grid, 256, 0, s>>>(a);
     else conv_gemm_kernel<BM, BN, WM, WN, 3, false><<<grid, 256, 0, s>>>(a);
   } else {
-    if (ks == 1) conv_gemm_dma_kernel<BM, BN, WM, WN, 1, false><<<grid, 256, 0, s>>>(a);
-    else if (tapu) conv_gemm_dma_kernel<BM, BN, WM, WN, 3, true><<<grid, 256, 0, s>>>(a);
-    else conv_gemm_dma_kernel<BM, BN, WM, WN, 3, false><<<grid, 256, 0, s>>>(a);
+    if (ks == 1) launch_dma<BM, BN, WM, WN, 1, false>(a, grid, s);
+    else if (tapu) launch_dma<BM, BN, WM, WN, 3, true>(a, grid, s);
+    else launch_dma<BM, BN, WM, WN, 3, false>(a, grid, s);
   }
 }
 
@@ -567,8 +625,13 @@ static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split
   a.rowvec_ld = d->rowvec_ld > 0 ? d->rowvec_ld : d->N;
   a.res = d->res; a.ldr = d->ldr; a.out_scale = d->out_scale == 0.f ? 1.f : d->out_scale; a.act = d->act;
   a.y = d->y; a.ldy = d->ldy; a.y_f32 = d->y_f32;
+  a.ablate = g_ablate;
   a.ktiles = d->K / 64;
   t = pick_tile(M, d->N, a.ktiles, d->split_k <= 0 && d->workspace != nullptr);
+  if (g_force_tile) {
+    static const int tb[5][2] = {{0, 0}, {128, 128}, {128, 64}, {64, 64}, {128, 32}};
+    t.bm = tb[g_force_tile][0]; t.bn = tb[g_force_tile][1]; t.split = g_force_split ? g_force_split : 1;
+  }
   a.ntm = cdiv(M, t.bm); a.ntn = cdiv(d->N, t.bn);
   split = d->split_k > 0 ? d->split_k : t.split;
   split = std::min(split, a.ktiles);
@@ -582,6 +645,17 @@ static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split
 }  // namespace ls
 
 using namespace ls;
+
+extern "C" int ls_set_tuning(int32_t key, int32_t value) {
+  switch (key) {
+    case 1: g_force_regstage = value != 0; return LS_OK;
+    case 2: if (value < 0 || value > 4) return fail(LS_ERR_INVALID, "tile id 0..4"); g_force_tile = value; return LS_OK;
+    case 3: g_force_split = value; return LS_OK;
+    case 4: g_ablate = value; return LS_OK;
+    case 5: if (value != 32 && value != 64) return fail(LS_ERR_INVALID, "BK 32 or 64"); g_bk = value; return LS_OK;
+    default: return fail(LS_ERR_INVALID, "ls_set_tuning: unknown key");
+  }
+}
 
 extern "C" size_t ls_conv_workspace_bytes(const ls_conv_desc* d) {
   ConvArgs a; TileCfg t; int split;

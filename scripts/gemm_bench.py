@@ -1,0 +1,50 @@
+"""Micro-benchmark of ls_conv2d on the UNet's contraction shapes (HIP events,
+median of N launches).  usage: python scripts/gemm_bench.py [regstage] [tile]"""
+import os, sys, statistics
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from latentsync_amd import ops, _lib
+from latentsync_amd.packing import pack_weight
+
+lib = _lib.load()
+SHAPES = [  # (name, n_img, H, Cin, Cout, ksize, act)
+    ("conv0 320->320 3x3", 16, 32, 320, 320, 3, 0), ("conv1 640->640 3x3", 16, 16, 640, 640, 3, 0),
+    ("conv2 1280 3x3", 16, 8, 1280, 1280, 3, 0), ("conv3 1280 3x3 4x4", 16, 4, 1280, 1280, 3, 0),
+    ("conv up0 960->320", 16, 32, 960, 320, 3, 0),
+    ("qkv0 320->960", 16, 32, 320, 960, 1, 0), ("geglu0 320->2560", 16, 32, 320, 2560, 1, 1),
+    ("ff2_0 1280->320", 16, 32, 1280, 320, 1, 0), ("out0 320->320", 16, 32, 320, 320, 1, 0),
+    ("geglu1 640->5120", 16, 16, 640, 5120, 1, 1), ("ff2_1 2560->640", 16, 16, 2560, 640, 1, 0),
+    ("geglu2 1280->10240", 16, 8, 1280, 10240, 1, 1), ("ff2_2 5120->1280", 16, 8, 5120, 1280, 1, 0),
+    ("qkv2 1280->3840", 16, 8, 1280, 3840, 1, 0), ("vae conv 128 256^2", 16, 256, 128, 128, 3, 0),
+    ("vae conv 512 32^2", 16, 32, 512, 512, 3, 0),
+]
+
+
+def run(tag, reps=20):
+    tot_f, tot_t = 0.0, 0.0
+    for name, n, H, cin, cout, ks, act in SHAPES:
+        x = torch.randn(n, H, H, cin, device="cuda").to(torch.bfloat16)
+        w = torch.randn(cout, cin, ks, ks) / (cin * ks * ks) ** 0.5
+        pw = ops.Packed(pack_weight(w).to(torch.bfloat16).cuda(), torch.zeros(cout, device="cuda"), cin, ks, cout,
+                        geglu=act == 1)
+        f = lambda: ops.conv(x, pw, act=act)
+        for _ in range(3):
+            f()
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(); f(); e1.record(); torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        t = statistics.median(ts)
+        fl = 2.0 * n * H * H * cout * cin * ks * ks
+        tot_f += fl; tot_t += t
+        print(f"{tag:10s} {name:24s} M={n*H*H:7d} N={cout:6d} K={cin*ks*ks:6d}  {t*1e3:8.1f} us  {fl/t/1e9:7.1f} TF/s")
+    print(f"{tag:10s} TOTAL {tot_t:.3f} ms  {tot_f/tot_t/1e9:.1f} TF/s")
+
+
+if __name__ == "__main__":
+    for mode in sys.argv[1:] or ["dma"]:
+        lib.ls_set_tuning(1, 1 if mode == "reg" else 0)
+        lib.ls_set_tuning(4, {"nomfma": 1, "nodma": 2}.get(mode, 0))
+        lib.ls_set_tuning(5, 32 if mode == "bk32" else 64)
+        run(mode)
