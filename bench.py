@@ -23,7 +23,7 @@ import torch.distributed as dist
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from latentsync_amd import ops  # noqa: E402
+from latentsync_amd import ops, shard  # noqa: E402
 from latentsync_amd.config import STAGE2_MODEL  # noqa: E402
 from latentsync_amd.pipeline import WindowEngine, load_fixed_mask  # noqa: E402
 from latentsync_amd.scheduler import DDIMScheduler  # noqa: E402
@@ -151,8 +151,8 @@ def main():
 
     K, W = args.steps, args.warmup
     FB = F * nw  # frames per step (batch of windows)
-    gathered = torch.empty((world * K * FB, R, R, 3), dtype=torch.uint8, device=device)
-    mine = torch.empty((K * FB, R, R, 3), dtype=torch.uint8, device=device)
+    # rank r owns windows r, r+N, ... of the job (shard.rank_windows); K*nw per rank
+    mine = torch.empty((K * nw, F, R, R, 3), dtype=torch.uint8, device=device)
     for _ in range(max(W, 1) if not args.no_graphs else W):
         eng.run()
     torch.cuda.synchronize(device)
@@ -168,11 +168,9 @@ def main():
         eng.run()
         e1.record(stream)
         ev_step.append((e0, e1))
-        mine[k * FB:(k + 1) * FB].copy_(eng.out_u8)
-    if world > 1:
-        dist.all_gather_into_tensor(gathered, mine)  # decoded frames over xGMI, once, at the end
-    else:
-        gathered.copy_(mine)
+        mine[k * nw:(k + 1) * nw].copy_(eng.out_u8.view(nw, F, R, R, 3))
+    # decoded frames of every rank back in clip order: ONE all-gather over xGMI, at the end
+    gathered = shard.gather_windows(mine, world * K * nw)
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()

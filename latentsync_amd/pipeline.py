@@ -25,7 +25,7 @@ import os
 import numpy as np
 import torch
 
-from . import ops
+from . import ops, shard
 
 SCALING = 0.18215
 
@@ -236,24 +236,36 @@ class LipsyncPipeline:
         outs, outs_u8 = [], []
         mask = mask.to(self.device, torch.float32)
         n_inf = math.ceil(n / num_frames)
+        # With torch.distributed initialised, rank r runs windows r, r+W, ... and the
+        # decoded frames are all-gathered once at the end (shard.py).  Every rank
+        # still draws every window's VAE noise so the result is independent of W.
+        world, rank = shard.world_and_rank()
+        mine = set(shard.rank_windows(n_inf, world, rank))
         for i in range(n_inf):
             sl = slice(i * num_frames, (i + 1) * num_frames)
-            fw = faces_u8[sl].to(self.device)
-            if fw.shape[0] != num_frames:
-                raise ValueError("the last window is short: pad the chunks to a multiple of num_frames "
-                                 "(pad_whisper_chunks_end, as the reference does)")
             if vae_noise is not None:
                 em, er = vae_noise(i)
             else:
                 em = torch.randn((num_frames, 4, h, h), generator=generator, device=self.device)
                 er = torch.randn((num_frames, 4, h, h), generator=generator, device=self.device)
+            if i not in mine:
+                continue
+            fw = faces_u8[sl].to(self.device)
+            if fw.shape[0] != num_frames:
+                raise ValueError("the last window is short: pad the chunks to a multiple of num_frames "
+                                 "(pad_whisper_chunks_end, as the reference does)")
             eng.load(fw, mask, whisper_chunks[sl].to(self.device), all_latents[:, :, sl], em, er)
             eng.run()
             outs.append(eng.out.clone())
             outs_u8.append(eng.out_u8.clone())
             if callback is not None:
                 callback(i, None, eng.lat)
-        return torch.cat(outs), torch.cat(outs_u8)
+        if world == 1:
+            return torch.cat(outs), torch.cat(outs_u8)
+        F_, dev = num_frames, self.device
+        loc = torch.stack(outs) if outs else torch.empty((0, F_, 3, R, R), device=dev)
+        loc8 = torch.stack(outs_u8) if outs_u8 else torch.empty((0, F_, R, R, 3), dtype=torch.uint8, device=dev)
+        return (shard.gather_windows(loc, n_inf).flatten(0, 1), shard.gather_windows(loc8, n_inf).flatten(0, 1))
 
     @torch.no_grad()
     def __call__(self, video_path, audio_path, video_out_path, video_mask_path=None, num_frames=16, video_fps=25,
