@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LS_ABI_VERSION 1
+#define LS_ABI_VERSION 2
 
 typedef enum {
   LS_OK = 0,
@@ -119,9 +119,11 @@ int ls_groupnorm_apply(const uint16_t* x1, const uint16_t* x2, int32_t C1, int32
  * whisper LayerNorm model.py:29-31).  Optional fused temporal positional
  * encoding add (VersatileAttention pos_encoder, motion_module.py:267-268):
  *   y[r, c] += pe[(r / pe_rows_per_frame) % pe_frames, c]   (pe fp32 [len][C]).
+ * x rows are ldx elements apart (ldx >= C, multiple of 8); y is dense [rows][C].
  */
-int ls_layernorm(const uint16_t* x, int64_t rows, int32_t C, float eps, const float* gamma, const float* beta,
-                 const float* pe, int32_t pe_rows_per_frame, int32_t pe_frames, uint16_t* y, void* stream);
+int ls_layernorm(const uint16_t* x, int64_t ldx, int64_t rows, int32_t C, float eps, const float* gamma,
+                 const float* beta, const float* pe, int32_t pe_rows_per_frame, int32_t pe_frames, uint16_t* y,
+                 void* stream);
 
 /*
  * Multi-head attention softmax(Q K^T * scale) V on MFMA with LDS-staged K/V
@@ -212,6 +214,24 @@ int ls_add_rows(const uint16_t* x, int64_t rows, int32_t C, int32_t ldx, const f
  * key 2 = force tile 0 auto, 1 128x128, 2 128x64, 3 64x64, 4 128x32; key 3 = split-K with key 2;
  * key 4 = ablation (1 skip MFMA, 2 skip operand DMA; timing only); key 5 = DMA K-tile depth 32 or 64. */
 int ls_set_tuning(int32_t key, int32_t value);
+
+/* Whisper log-mel spectrogram (whisper/audio.py:92-125: torch.stft n_fft 400, hop
+ * 160, periodic Hann, centre/reflect padding, last frame dropped, |X|^2, mel
+ * filterbank, log10 clamp 1e-10, clip-global max-8 floor, (x + 4) / 4).
+ * audio fp32 [n_samples] (16 kHz mono), filters fp32 [n_mels][201];
+ * out bf16 [t_pad][n_mels] frame-major, T = n_samples / 160 frames, zero for
+ * T <= t < t_pad (the transcribe segment pad, whisper/audio.py pad_or_trim).
+ * Workspace: ls_log_mel_workspace_bytes. */
+size_t ls_log_mel_workspace_bytes(int64_t n_samples, int32_t n_mels);
+int ls_log_mel(const float* audio, int64_t n_samples, const float* filters, int32_t n_mels, int64_t t_pad,
+               uint16_t* out, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Audio2Feature.feature2chunks / get_sliced_feature (audio2feature.py:24-49, 85-100):
+ * feat bf16 rows [T][layers][C] with row stride ld_row; chunk i, row j =
+ * feat[clamp(int(i * 50 / fps) - 2 * left + j / layers, 0, T - 1)][j % layers];
+ * out [n_chunks][(left + right + 1) * 2 * layers][C], bf16 or fp32 (out_f32). */
+int ls_audio_chunks(const uint16_t* feat, int64_t ld_row, int32_t T, int32_t layers, int32_t C, int32_t n_chunks,
+                    double fps, int32_t left, int32_t right, void* out, int32_t out_f32, void* stream);
 
 int ls_abi_version(void);
 const char* ls_last_error(void);

@@ -10,7 +10,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LS_HIP_LIB", os.path.join(HERE, "libls_hip.so"))
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 c_u16p = C.c_void_p
 c_vp = C.c_void_p
@@ -55,7 +55,7 @@ _SIGS = {
     "ls_groupnorm_workspace_bytes": (C.c_size_t, [C.c_int32, C.c_int32]),
     "ls_groupnorm_apply": (C.c_int, [c_vp, c_vp, C.c_int32, C.c_int32, C.c_int64, C.c_int64, c_vp, c_vp, C.c_int32,
                                      c_vp, c_vp]),
-    "ls_layernorm": (C.c_int, [c_vp, C.c_int64, C.c_int32, C.c_float, c_vp, c_vp, c_vp, C.c_int32, C.c_int32,
+    "ls_layernorm": (C.c_int, [c_vp, C.c_int64, C.c_int64, C.c_int32, C.c_float, c_vp, c_vp, c_vp, C.c_int32, C.c_int32,
                                c_vp, c_vp]),
     "ls_attention": (C.c_int, [C.POINTER(AttnDesc), c_vp]),
     "ls_small_linear": (C.c_int, [c_vp, C.c_int32, C.c_int32, c_vp, c_vp, C.c_int32, C.c_int32, c_vp, c_vp]),
@@ -70,6 +70,10 @@ _SIGS = {
     "ls_scale_latents": (C.c_int, [c_vp, C.c_int64, C.c_float, C.c_float, c_vp, C.c_int32, c_vp]),
     "ls_paste_back": (C.c_int, [c_vp, C.c_int32, c_vp, C.c_int32, c_vp, C.c_int32, C.c_int32, c_vp, c_vp, c_vp]),
     "ls_set_tuning": (C.c_int, [C.c_int32, C.c_int32]),
+    "ls_log_mel_workspace_bytes": (C.c_size_t, [C.c_int64, C.c_int32]),
+    "ls_log_mel": (C.c_int, [c_vp, C.c_int64, c_vp, C.c_int32, C.c_int64, c_vp, c_vp, C.c_size_t, c_vp]),
+    "ls_audio_chunks": (C.c_int, [c_vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_double,
+                                  C.c_int32, C.c_int32, c_vp, C.c_int32, c_vp]),
     "ls_add_rows": (C.c_int, [c_vp, C.c_int64, C.c_int32, C.c_int32, c_vp, C.c_int32, c_vp, C.c_int32, c_vp]),
 }
 

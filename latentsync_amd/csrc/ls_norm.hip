@@ -72,12 +72,12 @@ gn_stats_kernel(const u16* __restrict__ x1, const u16* __restrict__ x2, int C1, 
     const u16* src; int ld;
     if (c < C1) { src = x1 + c; ld = C1; } else { src = x2 + (c - C1); ld = C2; }
     long p = p0 + r;
-    for (; p + 3 * R < p1; p += 4 * R) {  // 4 loads in flight
-      uint4 u[4];
+    for (; p + 7 * R < p1; p += 8 * R) {  // 8 independent loads in flight per thread
+      uint4 u[8];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) u[t] = *(const uint4*)(src + (base + p + t * R) * ld);
+      for (int t = 0; t < 8; ++t) u[t] = *(const uint4*)(src + (base + p + t * R) * ld);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
+      for (int t = 0; t < 8; ++t) {
         float f[8];
         unpack8(u[t], f);
 #pragma unroll
@@ -114,34 +114,35 @@ gn_stats_kernel(const u16* __restrict__ x1, const u16* __restrict__ x2, int C1, 
       const double dk = mean - (double)kk[c];
       m2 += s2 - 2.0 * dk * s1 + n_c * dk * dk;
     }
-    GnPart o; o.n = n; o.mean = mean; o.m2 = m2; o.pad = 0;
-    part[((long)s * nsplit + split) * groups + g] = o;
+    // write-through (sc1) 8-byte stores: visible chip-wide without a release fence
+    unsigned long long* dst = (unsigned long long*)&part[((long)s * nsplit + split) * groups + g];
+    __hip_atomic_store(dst + 0, (unsigned long long)__double_as_longlong(n), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(dst + 1, (unsigned long long)__double_as_longlong(mean), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(dst + 2, (unsigned long long)__double_as_longlong(m2), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   }
-  // ---- publish this block's partials, take an arrival ticket
+  // ---- every storing wave drains, then one lane takes the arrival ticket
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned t = __hip_atomic_fetch_add(counters + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     is_last = (t == (unsigned)(nsplit - 1));
   }
   __syncthreads();
   if (!is_last) return;
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    counters[s] = 0;  // re-arm for the next call (every block of this sample has arrived)
-  }
-  __syncthreads();
+  if (tid == 0) __hip_atomic_store(counters + s, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
   // ---- merge the splits: L lanes per group, Chan merge, shuffle tree
   const int L = groups > 32 ? 4 : 8;  // lanes per group (power of two, inside one wave)
   const int g = tid / L, j = tid % L;
   double n = 0.0, mean = 0.0, m2 = 0.0;
   if (g < groups) {
-    for (int i = j; i < nsplit; i += L) {
-      const GnPart pp = part[((long)s * nsplit + i) * groups + g];
-      chan_merge(n, mean, m2, pp.n, pp.mean, pp.m2);
+    for (int i = j; i < nsplit; i += L) {  // sc1 loads (L1 bypass) of the write-through partials
+      unsigned long long* src = (unsigned long long*)&part[((long)s * nsplit + i) * groups + g];
+      const double pn = __longlong_as_double((long long)__hip_atomic_load(src + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      const double pm = __longlong_as_double((long long)__hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      const double pq = __longlong_as_double((long long)__hip_atomic_load(src + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      chan_merge(n, mean, m2, pn, pm, pq);
     }
   }
   for (int off = 1; off < L; off <<= 1) {
@@ -163,11 +164,13 @@ gn_stats_kernel(const u16* __restrict__ x1, const u16* __restrict__ x2, int C1, 
 }
 
 static int gn_nsplit(int n_samples, long pps, int C) {
-  const long elems = pps * C;
-  long ns = elems / 65536;                        // >= 64K elements (128 KB) per block
-  ns = std::min<long>(ns, cdiv(512, n_samples));  // <= ~512 blocks in total
-  ns = std::min<long>(ns, pps / 8);
-  return (int)std::max<long>(1, std::min<long>(ns, 256));
+  // each thread should issue one batch of 8 independent 16-B loads: pixels per
+  // block ~ 8 x R (R = thread rows per channel chunk)
+  const int CC = C / 8;
+  const int R = CC <= GN_THREADS ? GN_THREADS / CC : 1;
+  long ns = pps / (8L * R);
+  ns = std::min<long>(ns, cdiv(8192, n_samples));
+  return (int)std::max<long>(1, std::min<long>(ns, 1024));
 }
 
 // Materialised GroupNorm apply (+SiLU) over an optional channel concat.
@@ -199,14 +202,14 @@ __global__ void gn_apply_kernel(const u16* __restrict__ x1, const u16* __restric
 // registers, two-pass mean / variance, 16-lane shuffle reductions.
 template <int NCH>
 __global__ void __launch_bounds__(256)
-layernorm_kernel(const u16* __restrict__ x, long rows, int C, float eps, const float* __restrict__ gamma,
+layernorm_kernel(const u16* __restrict__ x, long ldx, long rows, int C, float eps, const float* __restrict__ gamma,
                  const float* __restrict__ beta, const float* __restrict__ pe, int pe_rpf, int pe_frames,
                  u16* __restrict__ y) {
   const int sub = threadIdx.x & 15;
   const long row = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
   const bool live = row < rows;
   const int CC = C / 8;
-  const u16* xr = x + (live ? row : 0) * C;
+  const u16* xr = x + (live ? row : 0) * ldx;
   float v[NCH][8];
   float s = 0.f;
 #pragma unroll
@@ -260,7 +263,7 @@ layernorm_kernel(const u16* __restrict__ x, long rows, int C, float eps, const f
 using namespace ls;
 
 extern "C" size_t ls_groupnorm_workspace_bytes(int32_t n_samples, int32_t groups) {
-  return GN_COUNTER_BYTES + (size_t)n_samples * 512 * groups * sizeof(GnPart);
+  return GN_COUNTER_BYTES + (size_t)(8192 + n_samples) * groups * sizeof(GnPart);  // sum_s nsplit <= 8192 + n_samples
 }
 
 extern "C" int ls_groupnorm(const uint16_t* x1, const uint16_t* x2, int32_t C1, int32_t C2, int32_t n_samples,
@@ -299,26 +302,26 @@ extern "C" int ls_groupnorm_apply(const uint16_t* x1, const uint16_t* x2, int32_
 }
 
 template <int NCH>
-static void launch_ln(const uint16_t* x, int64_t rows, int32_t C, float eps, const float* gamma, const float* beta,
+static void launch_ln(const uint16_t* x, int64_t ldx, int64_t rows, int32_t C, float eps, const float* gamma, const float* beta,
                       const float* pe, int32_t pe_rpf, int32_t pe_frames, uint16_t* y, hipStream_t s) {
-  layernorm_kernel<NCH><<<cdiv(rows, 16), 256, 0, s>>>(x, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y);
+  layernorm_kernel<NCH><<<cdiv(rows, 16), 256, 0, s>>>(x, ldx, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y);
 }
 
-extern "C" int ls_layernorm(const uint16_t* x, int64_t rows, int32_t C, float eps, const float* gamma,
-                            const float* beta, const float* pe, int32_t pe_rpf, int32_t pe_frames, uint16_t* y,
+extern "C" int ls_layernorm(const uint16_t* x, int64_t ldx, int64_t rows, int32_t C, float eps,
+                            const float* gamma, const float* beta, const float* pe, int32_t pe_rpf, int32_t pe_frames, uint16_t* y,
                             void* stream) {
-  if (!x || !y || !gamma || !beta || C % 8 || C > 16 * 8 * 16 || rows <= 0)
-    return fail(LS_ERR_INVALID, "ls_layernorm: bad arguments (C % 8 == 0, C <= 2048)");
+  if (!x || !y || !gamma || !beta || C % 8 || C > 16 * 8 * 16 || rows <= 0 || ldx < C || ldx % 8)
+    return fail(LS_ERR_INVALID, "ls_layernorm: bad arguments (C % 8 == 0, C <= 2048, ldx >= C, ldx % 8 == 0)");
   if (pe && (pe_rpf <= 0 || pe_frames <= 0)) return fail(LS_ERR_INVALID, "ls_layernorm: bad pe geometry");
   hipStream_t s = (hipStream_t)stream;
   const int nch = cdiv(C / 8, 16);
-  if (nch <= 1) launch_ln<1>(x, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
-  else if (nch <= 2) launch_ln<2>(x, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
-  else if (nch <= 3) launch_ln<3>(x, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
-  else if (nch <= 5) launch_ln<5>(x, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
-  else if (nch <= 8) launch_ln<8>(x, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
-  else if (nch <= 10) launch_ln<10>(x, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
-  else if (nch <= 12) launch_ln<12>(x, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
-  else launch_ln<16>(x, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
+  if (nch <= 1) launch_ln<1>(x, ldx, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
+  else if (nch <= 2) launch_ln<2>(x, ldx, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
+  else if (nch <= 3) launch_ln<3>(x, ldx, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
+  else if (nch <= 5) launch_ln<5>(x, ldx, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
+  else if (nch <= 8) launch_ln<8>(x, ldx, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
+  else if (nch <= 10) launch_ln<10>(x, ldx, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
+  else if (nch <= 12) launch_ln<12>(x, ldx, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
+  else launch_ln<16>(x, ldx, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
   return check_launch("layernorm_kernel");
 }

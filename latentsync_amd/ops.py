@@ -28,7 +28,7 @@ class Workspace:
     """Fixed-size per-device scratch (split-K partials, GroupNorm partials).  Never
     re-allocated after creation so captured graphs keep valid pointers."""
 
-    def __init__(self, device, gemm_bytes=256 << 20, gn_bytes=16 << 20):
+    def __init__(self, device, gemm_bytes=256 << 20, gn_bytes=24 << 20):
         self.gemm = torch.empty(gemm_bytes, dtype=torch.uint8, device=device)
         self.gn = torch.zeros(gn_bytes, dtype=torch.uint8, device=device)  # GN arrival counters start at 0
 
@@ -52,6 +52,19 @@ class Packed:
         self.N, self.K = w.shape
         self.n_out = n_out
         self.geglu = geglu
+
+
+def _ld(t):
+    """Pixel stride of an NHWC view (n, H, W, C): pixel p = (img*H + y)*W + x must
+    live at p * ld (channels contiguous)."""
+    n, H, W, C_ = t.shape
+    st = t.stride()
+    ld = st[2] if W > 1 else (st[1] if H > 1 else (st[0] if n > 1 else C_))
+    ok = (C_ == 1 or st[3] == 1) and (W == 1 or st[2] == ld) and (H == 1 or st[1] == W * ld) and \
+        (n == 1 or st[0] == H * W * ld)
+    if not ok:
+        raise ValueError(f"NHWC view with non-uniform pixel strides {tuple(st)} for shape {tuple(t.shape)}")
+    return ld
 
 
 def conv(x, pw: Packed, *, x2=None, aff=None, stride=1, pad=None, upsample=False, out_hw=None, rowvec=None,
@@ -78,7 +91,7 @@ def conv(x, pw: Packed, *, x2=None, aff=None, stride=1, pad=None, upsample=False
     ws = workspace(x.device)
     d = _lib.ConvDesc()
     d.x1, d.x2, d.C1, d.C2 = _p(x), _p(x2), C1, C2
-    d.ld1, d.ld2 = C1, C2
+    d.ld1, d.ld2 = _ld(x), (_ld(x2) if x2 is not None else 0)
     d.n_img, d.H, d.W, d.Ho, d.Wo = n, H, W, Ho, Wo
     d.ksize, d.stride, d.pad, d.upsample = ks, stride, pad, int(upsample)
     if aff is not None:
@@ -88,10 +101,11 @@ def conv(x, pw: Packed, *, x2=None, aff=None, stride=1, pad=None, upsample=False
     if rowvec is not None:
         d.rowvec, d.rows_per_vec, d.rowvec_ld = _p(rowvec[0]), rowvec[1], rowvec[2]
     if res is not None:
-        d.res, d.ldr = _p(res), res.shape[-1]
+        d.res, d.ldr = _p(res), (_ld(res) if res.dim() == 4 else res.stride(-2))
     d.out_scale = out_scale
     d.act = act
-    d.y, d.ldy, d.y_f32 = _p(out), out.shape[-1], int(out.dtype == torch.float32)
+    assert tuple(out.shape) == (n, Ho, Wo, n_out), (tuple(out.shape), (n, Ho, Wo, n_out))
+    d.y, d.ldy, d.y_f32 = _p(out), _ld(out), int(out.dtype == torch.float32)
     d.split_k = split_k
     d.workspace, d.workspace_bytes = _p(ws.gemm), ws.gemm.numel()
     check(lib.ls_conv2d(C.byref(d), _stream()), "ls_conv2d")
@@ -99,10 +113,14 @@ def conv(x, pw: Packed, *, x2=None, aff=None, stride=1, pad=None, upsample=False
 
 
 def linear(x2d, pw: Packed, **kw):
-    """Token-row linear: x2d (rows, C) -> (rows, n_out)."""
+    """Token-row linear: x2d (rows, C) -> (rows, n_out).  x2d / res / out may be
+    row-strided views (stride(1) == 1)."""
     rows = x2d.shape[0]
-    y = conv(x2d.view(1, 1, rows, x2d.shape[1]), pw, **kw)
-    return y.view(rows, y.shape[-1])
+    for k in ("res", "out"):
+        if kw.get(k) is not None and kw[k].dim() == 2:
+            kw[k] = kw[k].unsqueeze(0).unsqueeze(0)
+    y = conv(x2d.unsqueeze(0).unsqueeze(0), pw, **kw)
+    return y.view(rows, y.shape[-1]) if y.is_contiguous() else y[0, 0]
 
 
 def group_norm(x, groups, eps, gamma, beta, n_samples, x2=None):
@@ -136,10 +154,12 @@ def affine_act(x, scale, shift, n_samples, silu):
 
 
 def layer_norm(x2d, gamma, beta, eps=1e-5, pe=None, pe_rows_per_frame=1, pe_frames=1):
+    """x2d (rows, C), rows may be strided (x2d.stride(1) == 1); y dense (rows, C)."""
     lib = _lib.load()
     rows, C_ = x2d.shape
-    y = torch.empty_like(x2d)
-    check(lib.ls_layernorm(_p(x2d), rows, C_, eps, _p(gamma), _p(beta), _p(pe), pe_rows_per_frame, pe_frames, _p(y),
+    assert x2d.stride(1) == 1
+    y = torch.empty((rows, C_), dtype=x2d.dtype, device=x2d.device)
+    check(lib.ls_layernorm(_p(x2d), x2d.stride(0), rows, C_, eps, _p(gamma), _p(beta), _p(pe), pe_rows_per_frame, pe_frames, _p(y),
                            _stream()), "ls_layernorm")
     return y
 

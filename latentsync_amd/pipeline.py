@@ -292,7 +292,8 @@ class LipsyncPipeline:
         if faces.shape[-1] != R:
             raise NotImplementedError("face resize needs torchvision (out of scope): store faces at the resolution")
         keep = load_fixed_mask(R, mask_image_path)
-        audio_samples = self.audio_encoder.read_audio(audio_path, audio_sample_rate)
+        from .audio import read_audio
+        audio_samples = read_audio(audio_path, audio_sample_rate)
         feat = self.audio_encoder.audio2feat(audio_path)
         chunks = self.audio_encoder.feature2chunks(feature_array=feat, fps=video_fps)
         shape = chunks[0].shape
