@@ -158,6 +158,7 @@ __device__ __forceinline__ int swz(int row, int ch) { return row * 8 + (ch ^ ((r
 template <int BM, int BN, int WM, int WN>
 __device__ __forceinline__ void store_tile(const ConvArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16], float* st,
                                            int m0, int n0, int z) {
+  constexpr int NT = WM * WN * 64;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int FM = WTM / 16, FN = WTN / 16;
   constexpr int SP = BN + 4;
@@ -180,7 +181,7 @@ __device__ __forceinline__ void store_tile(const ConvArgs& a, f32x4 (&acc)[BM / 
     const int rbase = m0 + p * WTM;
     if (a.split > 1) {
       float* P = a.partial + (long)z * a.M * a.N;
-      for (int q = tid; q < WTM * (BN / 8); q += 256) {
+      for (int q = tid; q < WTM * (BN / 8); q += NT) {
         const int r = q / (BN / 8), c8 = (q - r * (BN / 8)) * 8;
         const int row = rbase + r, col = n0 + c8;
         if (row >= a.M || col >= a.N) continue;
@@ -193,7 +194,7 @@ __device__ __forceinline__ void store_tile(const ConvArgs& a, f32x4 (&acc)[BM / 
         }
       }
     } else if (geglu) {
-      for (int q = tid; q < WTM * (BN / 16); q += 256) {
+      for (int q = tid; q < WTM * (BN / 16); q += NT) {
         const int r = q / (BN / 16), o8 = (q - r * (BN / 16)) * 8;
         const int ph = (o8 >> 4) * 32 + (o8 & 15);
         const int row = rbase + r, col = n0 + ph;
@@ -205,7 +206,7 @@ __device__ __forceinline__ void store_tile(const ConvArgs& a, f32x4 (&acc)[BM / 
         epi_geglu8(a, row, col, h, g, vec);
       }
     } else {
-      for (int q = tid; q < WTM * (BN / 8); q += 256) {
+      for (int q = tid; q < WTM * (BN / 8); q += NT) {
         const int r = q / (BN / 8), c8 = (q - r * (BN / 8)) * 8;
         const int row = rbase + r, col = n0 + c8;
         if (col >= a.N) continue;
@@ -496,6 +497,137 @@ __global__ void __launch_bounds__(256) conv_gemm_dma_kernel(ConvArgs a) {
   store_tile<BM, BN, WM, WN>(a, acc, (float*)lds, m0, n0, z);
 }
 
+// 256-row tile, 8 waves (2 M x 4 N), each wave 128 x BN/4 (FM = 8 fragments of
+// 16 rows x FN of 16 cols): 1.5x the MFMAs per LDS fragment read of the 4-wave
+// 64 x 64 wave tile.  One block per CU (128 KB of LDS: two 64-KB stages at
+// BN = 256), glds operand DMA into XOR-swizzled lane-linear images, one raw
+// barrier per K-tile; the next tile's DMA is issued right after the barrier so
+// it has a whole K-tile of MFMAs to land.  MFMA runs are bracketed by
+// s_setprio(1) so the co-resident wave's fragment reads interleave.
+template <int BN, int KS, bool TAPU>
+__global__ void __launch_bounds__(512) conv_gemm_big_kernel(ConvArgs a) {
+  constexpr int BM = 256, BK = 64, WM = 2, WN = 4;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int FM = WTM / 16, FN = WTN / 16, FH = FM / 2;
+  constexpr int CPR = BK / 8;
+  constexpr int AI = BM * CPR / 512, BI = BN * CPR / 512;
+  constexpr int STAGE = (BM + BN) * CPR;
+  extern __shared__ __attribute__((aligned(16))) uint4 lds_dyn[];
+  uint4* lds = lds_dyn;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int nt = a.ntm * a.ntn;
+  int bid = xcd_remap(blockIdx.x, nt * a.split);
+  const int z = bid / nt;
+  bid -= z * nt;
+  const int tm = bid / a.ntn, tn = bid - tm * a.ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kt0 = z * a.kt_per_split;
+  const int kt1 = min(a.ktiles, kt0 + a.kt_per_split);
+
+  int arow[AI], ach[AI], brow[BI], bch[BI];
+  RowGeo geo[AI];
+#pragma unroll
+  for (int p = 0; p < AI; ++p) {
+    const int q = (wid * AI + p) * 64 + lane;
+    const int row = q / CPR;
+    arow[p] = m0 + row;
+    ach[p] = swz_bk<BK>(row, q % CPR) - row * CPR;
+    if (KS == 3) {
+      const int m = m0 + row;
+      const int hw = a.Ho * a.Wo;
+      const int n = m / hw, r = m - n * hw;
+      const int yo = r / a.Wo, xo = r - yo * a.Wo;
+      geo[p].pb = n * a.H * a.W;
+      geo[p].yb = (m < a.M) ? (a.upsample ? yo - a.pad : yo * a.stride - a.pad) : -(1 << 28);
+      geo[p].xb = a.upsample ? xo - a.pad : xo * a.stride - a.pad;
+    } else {
+      geo[p].pb = 0; geo[p].yb = 0; geo[p].xb = 0;
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < BI; ++p) {
+    const int q = (wid * BI + p) * 64 + lane;
+    const int row = q / CPR;
+    brow[p] = n0 + row;
+    bch[p] = swz_bk<BK>(row, q % CPR) - row * CPR;
+  }
+  auto issue = [&](int kt, int stage) {
+    uint4* base = lds + stage * STAGE;
+#pragma unroll
+    for (int p = 0; p < AI; ++p)
+      glds16(a_src<KS, TAPU, BK>(a, kt, ach[p], arow[p], geo[p]), base + (wid * AI + p) * 64);
+#pragma unroll
+    for (int p = 0; p < BI; ++p) {
+      const void* src = brow[p] < a.N ? (const void*)(a.w + (long)brow[p] * a.K + kt * BK + bch[p] * 8)
+                                      : (const void*)ls_zero_page;
+      glds16(src, base + BM * CPR + (wid * BI + p) * 64);
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  if (kt0 < kt1) issue(kt0, 0);
+  int stage = 0;
+  for (int kt = kt0; kt < kt1; ++kt) {
+    wait_vm<0>();  // this wave's share of tile kt has landed
+    __builtin_amdgcn_s_barrier();  // ... everyone's, and stage^1 is no longer read
+    asm volatile("" ::: "memory");
+    if (kt + 1 < kt1) issue(kt + 1, stage ^ 1);
+    const uint4* cur = lds + stage * STAGE;
+    bf16x8 bfr[2][FN], af[2][FH];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = ks * 4 + (lane >> 4);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bfr[ks][j] = __builtin_bit_cast(bf16x8, cur[BM * CPR + swz_bk<BK>(wn * WTN + j * 16 + (lane & 15), c)]);
+#pragma unroll
+      for (int i = 0; i < FH; ++i)
+        af[ks][i] = __builtin_bit_cast(bf16x8, cur[swz_bk<BK>(wm * WTM + i * 16 + (lane & 15), c)]);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 an[2][FH];
+      if (h == 0) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int c = ks * 4 + (lane >> 4);
+#pragma unroll
+          for (int i = 0; i < FH; ++i)
+            an[ks][i] = __builtin_bit_cast(bf16x8, cur[swz_bk<BK>(wm * WTM + (FH + i) * 16 + (lane & 15), c)]);
+        }
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < FH; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[h * FH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bfr[ks][j], acc[h * FH + i][j],
+                                                                          0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (h == 0) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int i = 0; i < FH; ++i) af[ks][i] = an[ks][i];
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    stage ^= 1;
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  store_tile<BM, BN, WM, WN>(a, acc, (float*)lds, m0, n0, z);
+}
+
 // split-K reduction + epilogue: one thread per 8 output columns
 __global__ void splitk_reduce_kernel(ConvArgs a) {
   const bool geglu = a.act == LS_ACT_GEGLU;
@@ -584,6 +716,25 @@ static void launch_dma(const ConvArgs& a, int grid, hipStream_t s) {
   launch_dma1<BM, BN, WM, WN, KS, TAPU, 2, 64>(a, grid, s);
 }
 
+template <int BN, int KS, bool TAPU>
+static void launch_big1(const ConvArgs& a, int grid, hipStream_t s) {
+  const size_t shm = std::max<size_t>((size_t)2 * (256 + BN) * 8 * 16, (size_t)128 * (BN + 4) * 4);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)conv_gemm_big_kernel<BN, KS, TAPU>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)shm);
+    attr = true;
+  }
+  conv_gemm_big_kernel<BN, KS, TAPU><<<grid, 512, shm, s>>>(a);
+}
+
+template <int BN>
+static void launch_big(const ConvArgs& a, int ks, bool tapu, int grid, hipStream_t s) {
+  if (ks == 1) launch_big1<BN, 1, false>(a, grid, s);
+  else if (tapu) launch_big1<BN, 3, true>(a, grid, s);
+  else launch_big1<BN, 3, false>(a, grid, s);
+}
+
 template <int BM, int BN, int WM, int WN>
 static void launch_cfg(const ConvArgs& a, int ks, bool tapu, int grid, hipStream_t s) {
   if (a.aff_scale || g_force_regstage) {  // prologue needs the register path
@@ -629,7 +780,7 @@ static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split
   a.ktiles = d->K / 64;
   t = pick_tile(M, d->N, a.ktiles, d->split_k <= 0 && d->workspace != nullptr);
   if (g_force_tile) {
-    static const int tb[5][2] = {{0, 0}, {128, 128}, {128, 64}, {64, 64}, {128, 32}};
+    static const int tb[7][2] = {{0, 0}, {128, 128}, {128, 64}, {64, 64}, {128, 32}, {256, 256}, {256, 128}};
     t.bm = tb[g_force_tile][0]; t.bn = tb[g_force_tile][1]; t.split = g_force_split ? g_force_split : 1;
   }
   a.ntm = cdiv(M, t.bm); a.ntn = cdiv(d->N, t.bn);
@@ -649,7 +800,7 @@ using namespace ls;
 extern "C" int ls_set_tuning(int32_t key, int32_t value) {
   switch (key) {
     case 1: g_force_regstage = value != 0; return LS_OK;
-    case 2: if (value < 0 || value > 4) return fail(LS_ERR_INVALID, "tile id 0..4"); g_force_tile = value; return LS_OK;
+    case 2: if (value < 0 || value > 6) return fail(LS_ERR_INVALID, "tile id 0..6"); g_force_tile = value; return LS_OK;
     case 3: g_force_split = value; return LS_OK;
     case 4: g_ablate = value; return LS_OK;
     case 5: if (value != 32 && value != 64) return fail(LS_ERR_INVALID, "BK 32 or 64"); g_bk = value; return LS_OK;
@@ -683,7 +834,10 @@ extern "C" int ls_conv2d(const ls_conv_desc* d, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const bool tapu = (d->ksize == 3) && (a.Cin % 64 == 0);
   const int grid = a.ntm * a.ntn * a.split;
-  if (t.bm == 128 && t.bn == 128) launch_cfg<128, 128, 2, 2>(a, d->ksize, tapu, grid, s);
+  if (t.bm == 256 && !a.aff_scale && !g_force_regstage) {
+    if (t.bn == 256) launch_big<256>(a, d->ksize, tapu, grid, s);
+    else launch_big<128>(a, d->ksize, tapu, grid, s);
+  } else if (t.bm == 128 && t.bn == 128) launch_cfg<128, 128, 2, 2>(a, d->ksize, tapu, grid, s);
   else if (t.bm == 128 && t.bn == 64) launch_cfg<128, 64, 2, 2>(a, d->ksize, tapu, grid, s);
   else if (t.bm == 128 && t.bn == 32) launch_cfg<128, 32, 4, 1>(a, d->ksize, tapu, grid, s);
   else launch_cfg<64, 64, 2, 2>(a, d->ksize, tapu, grid, s);

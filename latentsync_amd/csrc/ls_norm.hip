@@ -1,31 +1,27 @@
 // GroupNorm statistics (-> per-(sample, channel) affine consumed by the conv/GEMM
 // prologue) and LayerNorm, for gfx950.
 //
-// GroupNorm: numerically robust single read pass.  Block = (split, sample); each
-// thread owns a fixed 16-B channel chunk and walks pixels, accumulating shifted
-// sums S1 = sum(x - k_c), S2 = sum((x - k_c)^2) with k_c the block's first pixel
-// (no catastrophic cancellation when |mean| >> std).  The block folds its
-// per-channel sums into per-group (n, mean, M2) in double; the finalize kernel
-// merges the splits with Chan's formula and emits scale/shift per channel.
+// GroupNorm: numerically robust single read pass.  Every (sample, group) uses one
+// shift k_g = x[first pixel of the sample][first channel of the group], so the
+// shifted sums S1 = sum(x - k_g), S2 = sum((x - k_g)^2) of all blocks simply add
+// (no cancellation when |mean| >> std, no pairwise merges).  Block = (split,
+// sample): threads own 16-B channel chunks and walk pixels with 8 loads in
+// flight (enough blocks that the whole tensor is in flight at once); the block
+// reduces its per-thread sums to per-group fp64 (S1, S2) in parallel (8 lanes
+// per group + shuffles) and adds them into a per-(sample, group) fp64
+// accumulator with agent-scope atomics; the last-arriving block of the sample
+// (arrival ticket) reads the accumulator, re-zeroes it and writes the
+// per-channel affine.  (fp64 sums: the atomic order changes results only at the
+// 1e-16 level.)
 #include "ls_common.h"
 
 namespace ls {
 
 constexpr int GN_THREADS = 256;
+constexpr int GN_MAX_SAMPLES = 1024;
 constexpr size_t GN_COUNTER_BYTES = 4096;  // per-sample arrival tickets at the workspace start
 
-struct GnPart { double n, mean, m2, pad; };
-
-// Chan et al. merge of (n, mean, M2)
-__device__ __forceinline__ void chan_merge(double& n, double& mean, double& m2, double nb, double meanb, double m2b) {
-  if (nb <= 0) return;
-  const double nt = n + nb;
-  const double d = meanb - mean;
-  const double f = nb / nt;  // one fp64 division per merge
-  mean += d * f;
-  m2 += m2b + d * d * n * f;
-  n = nt;
-}
+struct GnPart { double s1, s2; };  // per-(sample, group) accumulator, zero between calls
 
 __device__ __forceinline__ double shfl_xor_d(double v, int m) {
   const long long b = __double_as_longlong(v);
@@ -33,19 +29,25 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-// One launch: per-(split, sample) shifted partial sums -> per-group (n, mean, M2);
-// the LAST block of a sample (arrival ticket) merges the splits and writes the
-// per-channel affine.  Publication follows the agent-scope release/acquire
-// recipe (every storing wave drains vmcnt, barrier, lane-0 release fence,
-// ticket; the last arriver acquires before reading the partials).
+__device__ __forceinline__ void st_wt(double* p, double v) {
+  __hip_atomic_store((unsigned long long*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_wt(const double* p) {
+  return __longlong_as_double(
+      (long long)__hip_atomic_load((unsigned long long*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
 __global__ void __launch_bounds__(GN_THREADS)
 gn_stats_kernel(const u16* __restrict__ x1, const u16* __restrict__ x2, int C1, int C2, long pps, int nsplit,
                 int groups, float eps, const float* __restrict__ gamma, const float* __restrict__ beta,
                 GnPart* part, unsigned* counters, float* __restrict__ scale, float* __restrict__ shift) {
-  extern __shared__ __attribute__((aligned(16))) float gsh[];  // [R][C] S1, [R][C] S2, k[C]
+  extern __shared__ __attribute__((aligned(16))) float gsh[];  // [R][C] S1, [R][C] S2
+  __shared__ float kg[64];
   __shared__ float mean_s[64], rstd_s[64];
   __shared__ int is_last;
   const int C = C1 + C2, CC = C / 8;
+  const int cpg = C / groups;
   const int split = blockIdx.x, s = blockIdx.y;
   const int tid = threadIdx.x;
   const long p0 = pps * split / nsplit, p1 = pps * (split + 1) / nsplit;
@@ -54,10 +56,9 @@ gn_stats_kernel(const u16* __restrict__ x1, const u16* __restrict__ x2, int C1, 
   if (CC <= GN_THREADS) { R = GN_THREADS / CC; nchunk = 1; } else { R = 1; nchunk = (CC + GN_THREADS - 1) / GN_THREADS; }
   float* S1 = gsh;
   float* S2 = gsh + (long)R * C;
-  float* kk = gsh + 2L * R * C;
-  for (int c = tid; c < C; c += GN_THREADS) {
-    const long pix = base + p0;
-    kk[c] = (p1 > p0) ? bf2f(c < C1 ? x1[pix * C1 + c] : x2[pix * C2 + (c - C1)]) : 0.f;
+  if (tid < groups) {
+    const int c = tid * cpg;
+    kg[tid] = bf2f(c < C1 ? x1[base * C1 + c] : x2[base * C2 + (c - C1)]);
   }
   __syncthreads();
   for (int q = 0; q < nchunk; ++q) {
@@ -68,7 +69,7 @@ gn_stats_kernel(const u16* __restrict__ x1, const u16* __restrict__ x2, int C1, 
     const int c = cc * 8;
     float a1[8], a2[8], k8[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { a1[j] = 0.f; a2[j] = 0.f; k8[j] = kk[c + j]; }
+    for (int j = 0; j < 8; ++j) { a1[j] = 0.f; a2[j] = 0.f; k8[j] = kg[(c + j) / cpg]; }
     const u16* src; int ld;
     if (c < C1) { src = x1 + c; ld = C1; } else { src = x2 + (c - C1); ld = C2; }
     long p = p0 + r;
@@ -94,35 +95,26 @@ gn_stats_kernel(const u16* __restrict__ x1, const u16* __restrict__ x2, int C1, 
     for (int j = 0; j < 8; ++j) { S1[(long)r * C + c + j] = a1[j]; S2[(long)r * C + c + j] = a2[j]; }
   }
   __syncthreads();
-  const int cpg = C / groups;
-  const double n_c = (double)(p1 - p0);
-  for (int g = tid; g < groups; g += GN_THREADS) {
-    double tot = 0.0;
-    for (int j = 0; j < cpg; ++j) {
-      const int c = g * cpg + j;
-      double s1 = 0.0;
-      for (int r = 0; r < R; ++r) s1 += S1[(long)r * C + c];
-      tot += n_c * kk[c] + s1;
+  // ---- block partial per group: L lanes per group, strided over (row, channel) entries
+  const int L = groups > 32 ? 4 : 8;
+  const int g = tid / L, j = tid % L;
+  const int Rv = (nchunk == 1) ? R : 1;
+  double b1 = 0.0, b2 = 0.0;
+  if (g < groups) {
+    const int ne = Rv * cpg;
+    for (int e = j; e < ne; e += L) {
+      const int r = e / cpg, c = g * cpg + (e - r * cpg);
+      b1 += (double)S1[(long)r * C + c];
+      b2 += (double)S2[(long)r * C + c];
     }
-    const double n = n_c * cpg;
-    const double mean = n > 0 ? tot / n : 0.0;
-    double m2 = 0.0;
-    for (int j = 0; j < cpg; ++j) {
-      const int c = g * cpg + j;
-      double s1 = 0.0, s2 = 0.0;
-      for (int r = 0; r < R; ++r) { s1 += S1[(long)r * C + c]; s2 += S2[(long)r * C + c]; }
-      const double dk = mean - (double)kk[c];
-      m2 += s2 - 2.0 * dk * s1 + n_c * dk * dk;
-    }
-    // write-through (sc1) 8-byte stores: visible chip-wide without a release fence
-    unsigned long long* dst = (unsigned long long*)&part[((long)s * nsplit + split) * groups + g];
-    __hip_atomic_store(dst + 0, (unsigned long long)__double_as_longlong(n), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(dst + 1, (unsigned long long)__double_as_longlong(mean), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(dst + 2, (unsigned long long)__double_as_longlong(m2), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
   }
-  // ---- every storing wave drains, then one lane takes the arrival ticket
+  for (int off = 1; off < L; off <<= 1) { b1 += shfl_xor_d(b1, off); b2 += shfl_xor_d(b2, off); }
+  if (g < groups && j == 0) {
+    GnPart* d = &part[(long)s * groups + g];
+    __hip_atomic_fetch_add(&d->s1, b1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(&d->s2, b2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // ---- the adds are complete (vmcnt drained by every wave), then one lane takes the ticket
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
@@ -132,27 +124,16 @@ gn_stats_kernel(const u16* __restrict__ x1, const u16* __restrict__ x2, int C1, 
   __syncthreads();
   if (!is_last) return;
   if (tid == 0) __hip_atomic_store(counters + s, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-  // ---- merge the splits: L lanes per group, Chan merge, shuffle tree
-  const int L = groups > 32 ? 4 : 8;  // lanes per group (power of two, inside one wave)
-  const int g = tid / L, j = tid % L;
-  double n = 0.0, mean = 0.0, m2 = 0.0;
-  if (g < groups) {
-    for (int i = j; i < nsplit; i += L) {  // sc1 loads (L1 bypass) of the write-through partials
-      unsigned long long* src = (unsigned long long*)&part[((long)s * nsplit + i) * groups + g];
-      const double pn = __longlong_as_double((long long)__hip_atomic_load(src + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      const double pm = __longlong_as_double((long long)__hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      const double pq = __longlong_as_double((long long)__hip_atomic_load(src + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      chan_merge(n, mean, m2, pn, pm, pq);
-    }
-  }
-  for (int off = 1; off < L; off <<= 1) {
-    const double nb = shfl_xor_d(n, off), mb = shfl_xor_d(mean, off), qb = shfl_xor_d(m2, off);
-    chan_merge(n, mean, m2, nb, mb, qb);
-  }
-  if (g < groups && j == 0) {
-    const double var = n > 0 ? m2 / n : 0.0;
-    mean_s[g] = (float)mean;
-    rstd_s[g] = (float)(1.0 / sqrt(var + (double)eps));
+  if (tid < groups) {
+    GnPart* d = &part[(long)s * groups + tid];
+    const double t1 = ld_wt(&d->s1), t2 = ld_wt(&d->s2);
+    st_wt(&d->s1, 0.0);  // re-zero for the next call
+    st_wt(&d->s2, 0.0);
+    const double n = (double)pps * cpg;
+    const double m1 = t1 / n;
+    const double var = fmax(t2 / n - m1 * m1, 0.0);
+    mean_s[tid] = (float)((double)kg[tid] + m1);
+    rstd_s[tid] = (float)(1.0 / sqrt(var + (double)eps));
   }
   __syncthreads();
   for (int c = tid; c < C; c += GN_THREADS) {
@@ -164,13 +145,12 @@ gn_stats_kernel(const u16* __restrict__ x1, const u16* __restrict__ x2, int C1, 
 }
 
 static int gn_nsplit(int n_samples, long pps, int C) {
-  // each thread should issue one batch of 8 independent 16-B loads: pixels per
-  // block ~ 8 x R (R = thread rows per channel chunk)
+  // ~8 pixel rows per thread (one batch of 8 loads in flight each), <= ~4096 blocks
   const int CC = C / 8;
   const int R = CC <= GN_THREADS ? GN_THREADS / CC : 1;
   long ns = pps / (8L * R);
-  ns = std::min<long>(ns, cdiv(8192, n_samples));
-  return (int)std::max<long>(1, std::min<long>(ns, 1024));
+  ns = std::min<long>(ns, std::max<long>(1, cdiv(4096, n_samples)));
+  return (int)std::max<long>(1, std::min<long>(ns, 4096));
 }
 
 // Materialised GroupNorm apply (+SiLU) over an optional channel concat.
@@ -263,7 +243,7 @@ layernorm_kernel(const u16* __restrict__ x, long ldx, long rows, int C, float ep
 using namespace ls;
 
 extern "C" size_t ls_groupnorm_workspace_bytes(int32_t n_samples, int32_t groups) {
-  return GN_COUNTER_BYTES + (size_t)(8192 + n_samples) * groups * sizeof(GnPart);  // sum_s nsplit <= 8192 + n_samples
+  return GN_COUNTER_BYTES + (size_t)n_samples * groups * sizeof(GnPart);
 }
 
 extern "C" int ls_groupnorm(const uint16_t* x1, const uint16_t* x2, int32_t C1, int32_t C2, int32_t n_samples,
@@ -274,14 +254,14 @@ extern "C" int ls_groupnorm(const uint16_t* x1, const uint16_t* x2, int32_t C1, 
     return fail(LS_ERR_INVALID, "ls_groupnorm: bad arguments");
   if (C1 % 8 || C2 % 8 || C % groups || groups > 64 || (C2 && !x2))
     return fail(LS_ERR_INVALID, "ls_groupnorm: channels must be multiples of 8 and groups <= 64");
-  if (n_samples > (int)(GN_COUNTER_BYTES / sizeof(unsigned)))
+  if (n_samples > GN_MAX_SAMPLES)
     return fail(LS_ERR_INVALID, "ls_groupnorm: too many samples");
   const int ns = gn_nsplit(n_samples, pps, C);
-  const size_t need = GN_COUNTER_BYTES + (size_t)n_samples * ns * groups * sizeof(GnPart);
+  const size_t need = ls_groupnorm_workspace_bytes(n_samples, groups);
   if (!workspace || workspace_bytes < need) return fail(LS_ERR_WORKSPACE, "ls_groupnorm: workspace too small");
   const int CC = C / 8;
   const int R = CC <= GN_THREADS ? GN_THREADS / CC : 1;
-  const size_t shm = (2 * (size_t)R * C + C) * sizeof(float);
+  const size_t shm = 2 * (size_t)R * C * sizeof(float);
   if (shm > 60 * 1024) return fail(LS_ERR_INVALID, "ls_groupnorm: too many channels");
   unsigned* counters = (unsigned*)workspace;  // zero-initialised by the caller once; re-armed by each call
   GnPart* part = (GnPart*)((char*)workspace + GN_COUNTER_BYTES);

@@ -20,9 +20,10 @@ SHAPES = [  # (name, n_img, H, Cin, Cout, ksize, act)
 ]
 
 
-def run(tag, reps=20):
+def run(tag, reps=20, scale=1):
     tot_f, tot_t = 0.0, 0.0
     for name, n, H, cin, cout, ks, act in SHAPES:
+        n = n * scale
         x = torch.randn(n, H, H, cin, device="cuda").to(torch.bfloat16)
         w = torch.randn(cout, cin, ks, ks) / (cin * ks * ks) ** 0.5
         pw = ops.Packed(pack_weight(w).to(torch.bfloat16).cuda(), torch.zeros(cout, device="cuda"), cin, ks, cout,
@@ -43,8 +44,11 @@ def run(tag, reps=20):
 
 
 if __name__ == "__main__":
-    for mode in sys.argv[1:] or ["dma"]:
+    # modes: dma reg nomfma nodma bk32 t1..t6 (forced tile id); suffix @4 = 4x the frames
+    for arg in sys.argv[1:] or ["dma"]:
+        mode, _, sc = arg.partition("@")
         lib.ls_set_tuning(1, 1 if mode == "reg" else 0)
         lib.ls_set_tuning(4, {"nomfma": 1, "nodma": 2}.get(mode, 0))
         lib.ls_set_tuning(5, 32 if mode == "bk32" else 64)
-        run(mode)
+        lib.ls_set_tuning(2, int(mode[1:]) if mode.startswith("t") else 0)
+        run(arg, scale=int(sc or 1))

@@ -223,3 +223,70 @@ def test_ddim_cfg_step(gpu):
     assert int(step.item()) == 4
     assert rel_err(unet_in[:P, :4].float().cpu(), ref) < 1e-2
     assert rel_err(unet_in[P:, :4].float().cpu(), ref) < 1e-2
+
+
+@pytest.fixture
+def forced_tile():
+    from latentsync_amd import _lib
+    lib = _lib.load()
+
+    def force(tile, split=0):
+        lib.ls_set_tuning(2, tile)
+        lib.ls_set_tuning(3, split)
+    yield force
+    lib.ls_set_tuning(2, 0)
+    lib.ls_set_tuning(3, 0)
+
+
+@pytest.mark.parametrize("tile", [1, 2, 3, 5, 6])
+@pytest.mark.parametrize("case", ["linear_res", "geglu", "conv3x3", "conv3x3_up_s2", "split2"])
+def test_gemm_tiles(gpu, forced_tile, tile, case):
+    """Every tile configuration of ls_conv2d (incl. the 8-wave 256-row kernel) on
+    ragged M / N, fused epilogues and TAPU 3x3 gathers.  Tolerance 1e-2 (bf16 out)."""
+    if case in ("linear_res", "geglu", "split2"):
+        M, K, N = 700, 640, (1024 if case == "geglu" else 320)
+        act = ops.ACT_GEGLU if case == "geglu" else 0
+        x = bf(rnd(M, K, seed=40))
+        w = bf(rnd(N, K, seed=41, scale=1 / math.sqrt(K)))
+        b = rnd(N, seed=42, scale=0.1)
+        forced_tile(tile, 2 if case == "split2" else 0)
+        if act:
+            h, g = (x @ w.T + b).chunk(2, -1)
+            ref = h * F.gelu(g)
+            y = ops.linear(x.to(torch.bfloat16).to(DEV), packed(w, b, 1, geglu=True), act=act)
+        else:
+            res = bf(rnd(M, N, seed=43))
+            ref = x @ w.T + b + res
+            y = ops.linear(x.to(torch.bfloat16).to(DEV), packed(w, b, 1), res=res.to(torch.bfloat16).to(DEV))
+        assert rel_err(y.float().cpu(), ref) < 1e-2
+    else:
+        up = case == "conv3x3_up_s2"
+        n, H, cin, cout = 5, 12, 128, 192
+        x = bf(rnd(n, cin, H, H, seed=44))
+        w = bf(rnd(cout, cin, 3, 3, seed=45, scale=1 / math.sqrt(9 * cin)))
+        b = rnd(cout, seed=46, scale=0.1)
+        forced_tile(tile)
+        if up:
+            ref = F.conv2d(F.interpolate(x, scale_factor=2.0, mode="nearest"), w, b, padding=1)
+            y = ops.conv(nhwc(x), packed(w, b, 3), upsample=True)
+            assert rel_err(nchw(y), ref) < 1e-2
+            ref = F.conv2d(x, w, b, stride=2, padding=1)
+            y = ops.conv(nhwc(x), packed(w, b, 3), stride=2)
+        else:
+            ref = F.conv2d(x, w, b, padding=1)
+            y = ops.conv(nhwc(x), packed(w, b, 3))
+        assert rel_err(nchw(y), ref) < 1e-2
+
+
+def test_linear_strided_views(gpu):
+    """Row-strided input / residual / output views (the Whisper stacked-layer layout)."""
+    M, C = 300, 384
+    X = bf(rnd(M, 3, C, seed=47)).to(torch.bfloat16).to(DEV)
+    w = bf(rnd(C, C, seed=48, scale=1 / math.sqrt(C)))
+    b = rnd(C, seed=49, scale=0.1)
+    ops.linear(X[:, 0], packed(w, b, 1), res=X[:, 1], out=X[:, 2])
+    Xc = X.float().cpu()
+    ref = Xc[:, 0] @ w.T + b + Xc[:, 1]
+    assert rel_err(Xc[:, 2], ref) < 1e-2
+    ln = ops.layer_norm(X[:, 1], torch.ones(C, device=DEV), torch.zeros(C, device=DEV))
+    assert rel_err(ln.float().cpu(), F.layer_norm(Xc[:, 1], (C,))) < 1e-2
