@@ -149,7 +149,7 @@ int ls_attention(const ls_attn_desc* d, void* stream);
 
 /*
  * Small-M linear in fp32: y[m, n] = sum_k act(x[m, k]) * W[n, k] + bias[n]
- * (x fp32, W bf16 [N][K]); pre-activation SiLU optional.  TimestepEmbedding
+ * (x fp32, W bf16 [N][K], 0 < M <= 1024, K <= 2048, K % 8 == 0); pre-activation SiLU optional.  TimestepEmbedding
  * (unet.py:382) and the batched time_emb_proj of every ResnetBlock3D
  * (resnet.py:190-194).
  */

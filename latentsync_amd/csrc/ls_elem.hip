@@ -34,34 +34,46 @@ __global__ void timestep_embed_kernel(const int* ts, const int* step, int B, int
   }
 }
 
-// y[m, n] = sum_k act(x[m, k]) * W[n, k] + b[n]; one wave per output column n.
+// y[m, n] = sum_k act(x[m, k]) * W[n, k] + b[n]; one wave per output column n,
+// rows in chunks of SL_ROWS per block (grid.y), the chunk's x cached in LDS.
+constexpr int SL_ROWS = 8;
 __global__ void __launch_bounds__(256) small_linear_kernel(const float* __restrict__ x, int M, int K,
                                                           const u16* __restrict__ w, const float* __restrict__ bias,
                                                           int N, int silu_in, float* __restrict__ y) {
-  extern __shared__ float xs[];  // [M][K]
-  for (int i = threadIdx.x; i < M * K; i += blockDim.x) {
-    const float v = x[i];
+  extern __shared__ float xs[];  // [SL_ROWS][K]
+  const int m0 = blockIdx.y * SL_ROWS;
+  const int mr = min(SL_ROWS, M - m0);
+  for (int i = threadIdx.x; i < mr * K; i += blockDim.x) {
+    const float v = x[(long)m0 * K + i];
     xs[i] = silu_in ? silu(v) : v;
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (n >= N) return;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  float acc[SL_ROWS];
+#pragma unroll
+  for (int mm = 0; mm < SL_ROWS; ++mm) acc[mm] = 0.f;
   const u16* wr = w + (long)n * K;
   for (int k = lane * 8; k < K; k += 512) {
     float f[8];
     unpack8(*(const uint4*)(wr + k), f);
-    for (int mm = 0; mm < M; ++mm) {
-      float s = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s += f[j] * xs[mm * K + k + j];
-      acc[mm] += s;
+    for (int mm = 0; mm < SL_ROWS; ++mm) {
+      if (mm < mr) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += f[j] * xs[mm * K + k + j];
+        acc[mm] += s;
+      }
     }
   }
-  for (int mm = 0; mm < M; ++mm) {
-    const float s = wave_sum(acc[mm]);
-    if (lane == 0) y[(long)mm * N + n] = s + (bias ? bias[n] : 0.f);
+#pragma unroll
+  for (int mm = 0; mm < SL_ROWS; ++mm) {
+    if (mm < mr) {
+      const float s = wave_sum(acc[mm]);
+      if (lane == 0) y[(long)(m0 + mm) * N + n] = s + (bias ? bias[n] : 0.f);
+    }
   }
 }
 
@@ -227,9 +239,11 @@ extern "C" int ls_timestep_embed(const int32_t* ts, const int32_t* step, int32_t
 
 extern "C" int ls_small_linear(const float* x, int32_t M, int32_t K, const uint16_t* w, const float* bias, int32_t N,
                                int32_t silu_in, float* y, void* stream) {
-  if (!x || !w || !y || M <= 0 || M > 4 || K % 8 || (size_t)M * K * 4 > 64 * 1024)
-    return fail(LS_ERR_INVALID, "ls_small_linear: M <= 4, K % 8 == 0, M*K <= 16384");
-  small_linear_kernel<<<cdiv(N, 4), 256, M * K * sizeof(float), (hipStream_t)stream>>>(x, M, K, w, bias, N, silu_in, y);
+  if (!x || !w || !y || M <= 0 || M > 1024 || K % 8 || K > 2048 || N <= 0)
+    return fail(LS_ERR_INVALID, "ls_small_linear: 0 < M <= 1024, K % 8 == 0, K <= 2048");
+  const int rows = std::min(M, SL_ROWS);
+  small_linear_kernel<<<dim3(cdiv(N, 4), cdiv(M, SL_ROWS)), 256, rows * K * sizeof(float), (hipStream_t)stream>>>(
+      x, M, K, w, bias, N, silu_in, y);
   return check_launch("small_linear_kernel");
 }
 

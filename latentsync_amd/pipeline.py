@@ -186,6 +186,9 @@ class LipsyncPipeline:
         self.vae, self.audio_encoder, self.denoising_unet, self.scheduler = vae, audio_encoder, denoising_unet, scheduler
         self.vae_scale_factor = 2 ** (len(self.vae.config.block_out_channels) - 1)
         self._engines = {}
+        # independent windows batched per UNet call (identical per-window math; see
+        # tests/test_gpu_pipeline.py::test_windows_batched_equal_separate)
+        self.windows_per_batch = 8
 
     @property
     def device(self):
@@ -206,11 +209,11 @@ class LipsyncPipeline:
             raise ValueError(f"`callback_steps` has to be a positive integer but is {callback_steps} of type"
                              f" {type(callback_steps)}.")
 
-    def engine(self, num_frames, resolution, steps, guidance_scale, use_graphs=True):
-        key = (num_frames, resolution, steps, float(guidance_scale), use_graphs)
+    def engine(self, num_frames, resolution, steps, guidance_scale, use_graphs=True, windows=1):
+        key = (num_frames, resolution, steps, float(guidance_scale), use_graphs, windows)
         if key not in self._engines:
             self._engines[key] = WindowEngine(self.denoising_unet, self.vae, self.scheduler, num_frames, resolution,
-                                              steps, guidance_scale, use_graphs)
+                                              steps, guidance_scale, use_graphs, windows=windows)
         return self._engines[key]
 
     def prepare_latents(self, num_frames, height, width, generator=None):
@@ -231,35 +234,42 @@ class LipsyncPipeline:
         n = whisper_chunks.shape[0]
         if all_latents is None:
             all_latents = self.prepare_latents(n, R, R, generator)
-        eng = self.engine(num_frames, R, num_inference_steps, guidance_scale)
         h = R // self.vae_scale_factor
         outs, outs_u8 = [], []
         mask = mask.to(self.device, torch.float32)
         n_inf = math.ceil(n / num_frames)
+        if n % num_frames:
+            raise ValueError("the last window is short: pad the chunks to a multiple of num_frames "
+                             "(pad_whisper_chunks_end, as the reference does)")
         # With torch.distributed initialised, rank r runs windows r, r+W, ... and the
         # decoded frames are all-gathered once at the end (shard.py).  Every rank
         # still draws every window's VAE noise so the result is independent of W.
         world, rank = shard.world_and_rank()
-        mine = set(shard.rank_windows(n_inf, world, rank))
+        mine = shard.rank_windows(n_inf, world, rank)
+        noise = {}
         for i in range(n_inf):
-            sl = slice(i * num_frames, (i + 1) * num_frames)
             if vae_noise is not None:
-                em, er = vae_noise(i)
+                noise[i] = vae_noise(i)
             else:
-                em = torch.randn((num_frames, 4, h, h), generator=generator, device=self.device)
-                er = torch.randn((num_frames, 4, h, h), generator=generator, device=self.device)
-            if i not in mine:
-                continue
-            fw = faces_u8[sl].to(self.device)
-            if fw.shape[0] != num_frames:
-                raise ValueError("the last window is short: pad the chunks to a multiple of num_frames "
-                                 "(pad_whisper_chunks_end, as the reference does)")
-            eng.load(fw, mask, whisper_chunks[sl].to(self.device), all_latents[:, :, sl], em, er)
+                noise[i] = (torch.randn((num_frames, 4, h, h), generator=generator, device=self.device),
+                            torch.randn((num_frames, 4, h, h), generator=generator, device=self.device))
+        # `windows_per_batch` of this rank's windows go through one UNet call per step
+        nb = max(1, int(self.windows_per_batch))
+        for b0 in range(0, len(mine), nb):
+            wins = mine[b0:b0 + nb]
+            eng = self.engine(num_frames, R, num_inference_steps, guidance_scale, windows=len(wins))
+            sls = [slice(i * num_frames, (i + 1) * num_frames) for i in wins]
+            cat = lambda xs: torch.cat([x.to(self.device) for x in xs])
+            eng.load(cat([faces_u8[sl] for sl in sls]), mask, cat([whisper_chunks[sl] for sl in sls]),
+                     cat([all_latents[:, :, sl] for sl in sls]),
+                     cat([noise[i][0] for i in wins]), cat([noise[i][1] for i in wins]))
             eng.run()
-            outs.append(eng.out.clone())
-            outs_u8.append(eng.out_u8.clone())
-            if callback is not None:
-                callback(i, None, eng.lat)
+            for k, i in enumerate(wins):
+                fs = slice(k * num_frames, (k + 1) * num_frames)
+                outs.append(eng.out[fs].clone())
+                outs_u8.append(eng.out_u8[fs].clone())
+                if callback is not None:
+                    callback(i, None, eng.lat)
         if world == 1:
             return torch.cat(outs), torch.cat(outs_u8)
         F_, dev = num_frames, self.device

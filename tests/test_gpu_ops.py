@@ -184,9 +184,10 @@ def test_attention_temporal_strided(gpu, C):
     assert rel_err(o.float().cpu(), o_ref) < 1.5e-2
 
 
-def test_small_linear_and_timestep(gpu):
+@pytest.mark.parametrize("M", [2, 8, 19])
+def test_small_linear_and_timestep(gpu, M):
     from oracle import ref_cpu as R
-    x = rnd(2, 1280, seed=70)
+    x = rnd(M, 1280, seed=70)
     w = bf(rnd(3000, 1280, seed=71, scale=1 / 36))
     b = rnd(3000, seed=72)
     y = ops.small_linear(x.to(DEV), w.to(torch.bfloat16).to(DEV), b.to(DEV), silu_in=True)

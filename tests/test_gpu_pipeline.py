@@ -44,3 +44,74 @@ def test_window_matches_oracle(gpu, guidance, graphs, monkeypatch):
     # outside the mouth the original pixels are pasted back exactly (up to bf16 of the prep)
     keep = mask.bool()[None, None].expand_as(ref)
     assert (out[keep] - ref[keep]).abs().max() < 1e-2
+
+
+def test_windows_batched_equal_separate(gpu, monkeypatch):
+    """Batching W independent windows through one UNet call per DDIM step (the
+    engine's `windows` option) computes each window as alone: per-window 5-D
+    GroupNorm / temporal attention, [uncond..., cond...] CFG layout.  Checked
+    against the fp32 oracle per window (3e-2, as the single-window test) and
+    against the single-window engine (3e-2: two bf16 runs whose GEMM tiling /
+    split-K differ; a mixed-up window or CFG half would be O(1))."""
+    Fr, Rr, steps, W = 8, 64, 2, 2
+    h = Rr // 8
+    unet = UNet3DConditionModel(**TINY_MODEL).init_weights(6).to("cuda").eval()
+    vae = AutoencoderKL(block_out_channels=(32, 64, 64, 64)).init_weights(7).to("cuda")
+    monkeypatch.setitem(R.VAE_CFG, "block_out_channels", (32, 64, 64, 64))
+    g = torch.Generator().manual_seed(8)
+    faces = (torch.rand((W * Fr, 3, Rr, Rr), generator=g) * 255).to(torch.uint8)
+    mask = load_fixed_mask(Rr)
+    audio = torch.randn((W * Fr, 50, 384), generator=g)
+    init = torch.randn((W, 4, 1, h, h), generator=g)
+    em, er = torch.randn((W * Fr, 4, h, h), generator=g), torch.randn((W * Fr, 4, h, h), generator=g)
+    sched = DDIMScheduler(**SCHED)
+    batched = WindowEngine(unet, vae, sched, Fr, Rr, steps, 2.0, windows=W)
+    batched.load(faces.cuda(), mask.cuda(), audio.cuda(), init.cuda(), em.cuda(), er.cuda())
+    out_b = batched.run().cpu()
+    for w in range(W):
+        sl = slice(w * Fr, (w + 1) * Fr)
+        ref = R.pipeline_window(unet.state_dict(), dict(unet.config), vae._sd, faces[sl], mask, audio[sl],
+                                init[w:w + 1], em[sl], er[sl], num_steps=steps, guidance_scale=2.0)
+        e = rel_err(out_b[sl], ref)
+        print("batched window vs oracle", w, e)
+        assert e < 3e-2
+    single = WindowEngine(unet, vae, sched, Fr, Rr, steps, 2.0, windows=1)
+    for w in range(W):
+        sl = slice(w * Fr, (w + 1) * Fr)
+        single.load(faces[sl].cuda(), mask.cuda(), audio[sl].cuda(), init[w:w + 1].cuda(), em[sl].cuda(),
+                    er[sl].cuda())
+        out_s = single.run().cpu()
+        e = rel_err(out_b[sl], out_s)
+        print("batched vs single window", w, e)
+        assert e < 3e-2
+
+
+def test_run_windows_batches_match_oracle(gpu, monkeypatch):
+    """LipsyncPipeline.run_windows over 3 windows with windows_per_batch = 2 (one
+    batch of 2 + one single) against the oracle window by window."""
+    from latentsync_amd.pipeline import LipsyncPipeline
+    Fr, Rr, steps, n_win = 8, 64, 2, 3
+    h = Rr // 8
+    unet = UNet3DConditionModel(**TINY_MODEL).init_weights(9).to("cuda").eval()
+    vae = AutoencoderKL(block_out_channels=(32, 64, 64, 64)).init_weights(10).to("cuda")
+    monkeypatch.setitem(R.VAE_CFG, "block_out_channels", (32, 64, 64, 64))
+    pipe = LipsyncPipeline(vae, None, unet, DDIMScheduler(**SCHED))
+    pipe.windows_per_batch = 2
+    g = torch.Generator().manual_seed(11)
+    N = n_win * Fr
+    faces = (torch.rand((N, 3, Rr, Rr), generator=g) * 255).to(torch.uint8)
+    mask = load_fixed_mask(Rr)
+    audio = torch.randn((N, 50, 384), generator=g)
+    init = torch.randn((1, 4, 1, h, h), generator=g).repeat(1, 1, N, 1, 1)
+    noise = [(torch.randn((Fr, 4, h, h), generator=g), torch.randn((Fr, 4, h, h), generator=g)) for _ in range(n_win)]
+    out, out_u8 = pipe.run_windows(faces, audio.cuda(), mask, Fr, steps, 1.0, all_latents=init.cuda(),
+                                   vae_noise=lambda i: (noise[i][0].cuda(), noise[i][1].cuda()))
+    assert out.shape == (N, 3, Rr, Rr) and out_u8.shape == (N, Rr, Rr, 3)
+    for w in range(n_win):
+        sl = slice(w * Fr, (w + 1) * Fr)
+        ref = R.pipeline_window(unet.state_dict(), dict(unet.config), vae._sd, faces[sl], mask, audio[sl],
+                                init[:, :, sl][:, :, :1], noise[w][0], noise[w][1], num_steps=steps,
+                                guidance_scale=1.0)
+        e = rel_err(out[sl].cpu(), ref)
+        print("run_windows window", w, e)
+        assert e < 3e-2
