@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LS_ABI_VERSION 2
+#define LS_ABI_VERSION 3
 
 typedef enum {
   LS_OK = 0,
@@ -62,7 +62,16 @@ enum { LS_ACT_NONE = 0, LS_ACT_GEGLU = 1, LS_ACT_GELU = 2, LS_ACT_SILU = 3 };
  *
  * Wp is the packed weight [N][K]: K = ksize*ksize*Cin rounded up to 64, tap-major
  * (see latentsync_amd/packing.py).  Epilogue, in this order:
- *   v = acc + bias[n] + rowvec[(m / rows_per_vec) * rowvec_ld + n]  (temb add, resnet.py:190-205)
+ *   if (ln_rowstats)  acc = rstd[m] * (acc - mean[m] * ln_colsum[n])
+ *       -- LayerNorm of the A rows folded into the GEMM: with Wp = W * gamma
+ *       (per input column), bias = b + W beta and ln_colsum[n] = sum_k Wp[n, k],
+ *       this equals W LN(x) + b exactly in real arithmetic (BasicTransformerBlock
+ *       norm1/2/3 -> to_q|k|v / to_q / ff.net.0, attention.py:145-199;
+ *       TemporalTransformerBlock norms -> q|k|v / FF, motion_module.py:240-313);
+ *       ln_rowstats = (mean, rstd) fp32 pairs per row from ls_row_stats
+ *   v = acc + bias[n] + rowvec[((m / rows_per_vec) % rowvec_mod) * rowvec_ld + n]
+ *       (temb add, resnet.py:190-205; W pe of the motion positional encoding;
+ *        rowvec_mod 0 = no modulo)
  *   v = (v + res[m, n]) * out_scale                      (residual, resnet.py:221)
  *   act: GEGLU pairs packed columns (32b+i, 32b+16+i) -> out col 16b+i,
  *        out = h * gelu_erf(g) (diffusers GEGLU); GELU (whisper MLP); SiLU.
@@ -84,6 +93,9 @@ typedef struct {
   void* y; int32_t ldy; int32_t y_f32;
   int32_t split_k;           /* 0 = choose automatically                       */
   void* workspace; size_t workspace_bytes;
+  const float* ln_rowstats;  /* NULL or (mean, rstd) per A row (ksize 1 only)  */
+  const float* ln_colsum;    /* [N] column sums of Wp (with ln_rowstats)       */
+  int32_t rowvec_mod;        /* 0 = none                                       */
 } ls_conv_desc;
 
 int ls_conv2d(const ls_conv_desc* d, void* stream);
@@ -124,6 +136,11 @@ int ls_groupnorm_apply(const uint16_t* x1, const uint16_t* x2, int32_t C1, int32
 int ls_layernorm(const uint16_t* x, int64_t ldx, int64_t rows, int32_t C, float eps, const float* gamma,
                  const float* beta, const float* pe, int32_t pe_rows_per_frame, int32_t pe_frames, uint16_t* y,
                  void* stream);
+
+/* Per-row LayerNorm statistics (mean, rstd = 1/sqrt(var + eps)) fp32 pairs of
+ * x [rows][C] (row pitch ldx): the producer side of the LayerNorm -> linear fold
+ * (ls_conv_desc.ln_rowstats). */
+int ls_row_stats(const uint16_t* x, int64_t ldx, int64_t rows, int32_t C, float eps, float* stats, void* stream);
 
 /*
  * Multi-head attention softmax(Q K^T * scale) V on MFMA with LDS-staged K/V

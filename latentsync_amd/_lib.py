@@ -10,7 +10,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LS_HIP_LIB", os.path.join(HERE, "libls_hip.so"))
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 c_u16p = C.c_void_p
 c_vp = C.c_void_p
@@ -33,6 +33,7 @@ class ConvDesc(C.Structure):
         ("y", c_vp), ("ldy", C.c_int32), ("y_f32", C.c_int32),
         ("split_k", C.c_int32),
         ("workspace", c_vp), ("workspace_bytes", C.c_size_t),
+        ("ln_rowstats", c_vp), ("ln_colsum", c_vp), ("rowvec_mod", C.c_int32),
     ]
 
 
@@ -57,6 +58,7 @@ _SIGS = {
                                      c_vp, c_vp]),
     "ls_layernorm": (C.c_int, [c_vp, C.c_int64, C.c_int64, C.c_int32, C.c_float, c_vp, c_vp, c_vp, C.c_int32, C.c_int32,
                                c_vp, c_vp]),
+    "ls_row_stats": (C.c_int, [c_vp, C.c_int64, C.c_int64, C.c_int32, C.c_float, c_vp, c_vp]),
     "ls_attention": (C.c_int, [C.POINTER(AttnDesc), c_vp]),
     "ls_small_linear": (C.c_int, [c_vp, C.c_int32, C.c_int32, c_vp, c_vp, C.c_int32, C.c_int32, c_vp, c_vp]),
     "ls_timestep_embed": (C.c_int, [c_vp, c_vp, C.c_int32, C.c_int32, C.c_int32, C.c_float, c_vp, c_vp]),

@@ -5,9 +5,10 @@ Whisper-tiny encoder on the HIP path.
       zero pad per 30 s segment: transcribe.py's segment loop + pad_or_trim)
   --conv1 (k3, GELU)--> --conv2 (k3 s2, GELU)--> + positional embedding
       -> X[:, 0]                                     (whisper/model.py:143-156)
-  4 x ResidualAttentionBlock: LN -> fused q|k|v GEMM -> flash attention (6 heads,
-      d 64, scale d^-1/2 = the reference's d^-1/4 on q and k) -> out GEMM
-      (+ residual) -> LN -> MLP GEMM (GELU) -> GEMM (+ residual) -> X[:, l]
+  4 x ResidualAttentionBlock: row stats -> fused q|k|v GEMM with attn_ln folded
+      in -> flash attention (6 heads, d 64, scale d^-1/2 = the reference's d^-1/4
+      on q and k) -> out GEMM (+ residual) -> row stats -> MLP GEMM (mlp_ln
+      folded, GELU) -> GEMM (+ residual) -> X[:, l]
                                                       (model.py:29-100, 158-171)
   X is [n_seg*1500][5][384] bf16: every layer writes its residual stream straight
   into its slot of the stacked `encoder_embeddings` (the include_embeddings
@@ -131,13 +132,14 @@ class _DeviceWhisper:
         for i in range(self.n_layer):
             p = f"encoder.blocks.{i}"
             qb, vb = sd[p + ".attn.query.bias"].float(), sd[p + ".attn.value.bias"].float()
+            # attn_ln / mlp_ln folded into the q|k|v and mlp.0 GEMMs (ls_conv_desc.ln_rowstats)
             blk = types.SimpleNamespace(
-                ln1=(dv.f32(p + ".attn_ln.weight"), dv.f32(p + ".attn_ln.bias")),
-                qkv=dv.packed(None, w=torch.cat([sd[p + f".attn.{n}.weight"].float() for n in ("query", "key", "value")]),
-                              b=torch.cat([qb, torch.zeros_like(qb), vb])),
+                qkv=dv.packed_ln(torch.cat([sd[p + f".attn.{n}.weight"].float() for n in ("query", "key", "value")]),
+                                 torch.cat([qb, torch.zeros_like(qb), vb]),
+                                 (sd[p + ".attn_ln.weight"], sd[p + ".attn_ln.bias"])),
                 out=dv.packed(p + ".attn.out.weight", p + ".attn.out.bias"),
-                ln2=(dv.f32(p + ".mlp_ln.weight"), dv.f32(p + ".mlp_ln.bias")),
-                mlp1=dv.packed(p + ".mlp.0.weight", p + ".mlp.0.bias"),
+                mlp1=dv.packed_ln(sd[p + ".mlp.0.weight"], sd[p + ".mlp.0.bias"],
+                                  (sd[p + ".mlp_ln.weight"], sd[p + ".mlp_ln.bias"])),
                 mlp2=dv.packed(p + ".mlp.2.weight", p + ".mlp.2.bias"))
             self.blocks.append(blk)
 
@@ -156,14 +158,12 @@ class _DeviceWhisper:
         for li, b in enumerate(self.blocks):
             x = X[:, li]
             y = X[:, li + 1]
-            t = ops.layer_norm(x, *b.ln1)
-            qkv = ops.linear(t, b.qkv)
+            qkv = ops.linear(x, b.qkv, ln_stats=ops.row_stats(x))
             qs = (ctx * 3 * C, 0, 3 * C, d)
             ops.attention(qkv, qkv[:, C:], qkv[:, 2 * C:], o, batch=n_seg, z2=1, heads=self.heads, nq=ctx, nk=ctx,
                           head_dim=d, qs=qs, ks=qs, vs=qs, os_=(ctx * C, 0, C, d))
             ops.linear(o, b.out, res=x, out=y)
-            t = ops.layer_norm(y, *b.ln2)
-            m = ops.linear(t, b.mlp1, act=ops.ACT_GELU)
+            m = ops.linear(y, b.mlp1, act=ops.ACT_GELU, ln_stats=ops.row_stats(y))
             ops.linear(m, b.mlp2, res=y, out=y)
         return X
 

@@ -22,7 +22,8 @@ struct ConvArgs {
   int n_img, H, W, Ho, Wo, stride, pad, upsample;
   const float* aff_scale; const float* aff_shift; int pix_per_sample; int silu_in;
   const u16* w; int K, N, M, CC;
-  const float* bias; const float* rowvec; int rows_per_vec, rowvec_ld;
+  const float* bias; const float* rowvec; int rows_per_vec, rowvec_ld, rowvec_mod;
+  const float* ln_mr; const float* ln_cs;
   const u16* res; int ldr; float out_scale; int act;
   void* y; int ldy; int y_f32;
   int ktiles, kt_per_split, split; float* partial;
@@ -48,12 +49,31 @@ __device__ __forceinline__ float act_fn(int act, float v) {
 
 // v[8] = accumulators of packed columns [col, col+8) of `row`; applies bias,
 // rowvec, residual, scale, activation and stores.  vec = all 8 in range and aligned.
+__device__ __forceinline__ long rv_row(const ConvArgs& a, int row) {
+  const int r = row / a.rows_per_vec;
+  return (long)(a.rowvec_mod ? r % a.rowvec_mod : r) * a.rowvec_ld;
+}
+
+// LayerNorm fold: acc = rstd * (acc - mean * colsum[c])
+__device__ __forceinline__ void ln_fold8(const ConvArgs& a, int row, int col, float* v, bool vec) {
+  const float2 mr = *(const float2*)(a.ln_mr + 2L * row);
+  if (vec) {
+    float cs[8];
+    load8f(a.ln_cs + col, cs);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = mr.y * (v[j] - mr.x * cs[j]);
+  } else {
+    for (int j = 0; j < 8 && col + j < a.N; ++j) v[j] = mr.y * (v[j] - mr.x * a.ln_cs[col + j]);
+  }
+}
+
 __device__ __forceinline__ void epi_chunk(const ConvArgs& a, int row, int col, float* v, bool vec) {
   if (row >= a.M) return;
+  if (a.ln_mr) ln_fold8(a, row, col, v, vec);
   if (vec) {
     float b[8], rv[8], rs[8];
     if (a.bias) load8f(a.bias + col, b); else for (int j = 0; j < 8; ++j) b[j] = 0.f;
-    if (a.rowvec) load8f(a.rowvec + (long)(row / a.rows_per_vec) * a.rowvec_ld + col, rv);
+    if (a.rowvec) load8f(a.rowvec + rv_row(a, row) + col, rv);
     else for (int j = 0; j < 8; ++j) rv[j] = 0.f;
     if (a.res) unpack8(*(const uint4*)(a.res + (long)row * a.ldr + col), rs);
     else for (int j = 0; j < 8; ++j) rs[j] = 0.f;
@@ -72,7 +92,7 @@ __device__ __forceinline__ void epi_chunk(const ConvArgs& a, int row, int col, f
       if (c >= a.N) break;
       float t = v[j];
       if (a.bias) t += a.bias[c];
-      if (a.rowvec) t += a.rowvec[(long)(row / a.rows_per_vec) * a.rowvec_ld + c];
+      if (a.rowvec) t += a.rowvec[rv_row(a, row) + c];
       if (a.res) t += bf2f(a.res[(long)row * a.ldr + c]);
       t = act_fn(a.act, t * a.out_scale);
       if (a.y_f32) ((float*)a.y)[(long)row * a.ldy + c] = t;
@@ -82,9 +102,13 @@ __device__ __forceinline__ void epi_chunk(const ConvArgs& a, int row, int col, f
 }
 
 // GEGLU chunk: h[8] = packed cols [ph, ph+8), g[8] = [ph+16, ph+24) -> out cols [oc, oc+8)
-__device__ __forceinline__ void epi_geglu8(const ConvArgs& a, int row, int ph, float* h, const float* g, bool vec) {
+__device__ __forceinline__ void epi_geglu8(const ConvArgs& a, int row, int ph, float* h, float* g, bool vec) {
   if (row >= a.M) return;
   const int oc = (ph >> 5) * 16 + (ph & 15);
+  if (a.ln_mr) {
+    ln_fold8(a, row, ph, h, true);
+    ln_fold8(a, row, ph + 16, g, true);
+  }
   float bh[8], bg[8];
   if (a.bias) { load8f(a.bias + ph, bh); load8f(a.bias + ph + 16, bg); }
   else for (int j = 0; j < 8; ++j) { bh[j] = 0.f; bg[j] = 0.f; }
@@ -772,7 +796,9 @@ static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split
   a.aff_scale = d->aff_scale; a.aff_shift = d->aff_shift;
   a.pix_per_sample = d->imgs_per_sample * d->H * d->W; a.silu_in = d->silu_in;
   a.w = d->w; a.K = d->K; a.N = d->N; a.M = (int)M; a.CC = Cin / 8;
-  a.bias = d->bias; a.rowvec = d->rowvec; a.rows_per_vec = d->rows_per_vec;
+  a.bias = d->bias; a.rowvec = d->rowvec; a.rows_per_vec = d->rows_per_vec; a.rowvec_mod = d->rowvec_mod;
+  a.ln_mr = d->ln_rowstats; a.ln_cs = d->ln_colsum;
+  if (a.ln_mr && (!a.ln_cs || d->ksize != 1)) return fail(LS_ERR_INVALID, "ls_conv2d: ln_rowstats needs ln_colsum, ksize 1");
   a.rowvec_ld = d->rowvec_ld > 0 ? d->rowvec_ld : d->N;
   a.res = d->res; a.ldr = d->ldr; a.out_scale = d->out_scale == 0.f ? 1.f : d->out_scale; a.act = d->act;
   a.y = d->y; a.ldy = d->ldy; a.y_f32 = d->y_f32;

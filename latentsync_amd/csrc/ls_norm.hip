@@ -184,7 +184,7 @@ template <int NCH>
 __global__ void __launch_bounds__(256)
 layernorm_kernel(const u16* __restrict__ x, long ldx, long rows, int C, float eps, const float* __restrict__ gamma,
                  const float* __restrict__ beta, const float* __restrict__ pe, int pe_rpf, int pe_frames,
-                 u16* __restrict__ y) {
+                 u16* __restrict__ y, float* __restrict__ stats) {
   const int sub = threadIdx.x & 15;
   const long row = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
   const bool live = row < rows;
@@ -217,6 +217,10 @@ layernorm_kernel(const u16* __restrict__ x, long ldx, long rows, int C, float ep
   for (int o = 8; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, 16);
   const float rstd = rsqrtf(s2 / C + eps);
   if (!live) return;
+  if (stats) {  // statistics only (LayerNorm folded into the consumer GEMM)
+    if (sub == 0) *(float2*)(stats + 2 * row) = make_float2(mean, rstd);
+    return;
+  }
   const float* per = pe ? pe + (long)((row / pe_rpf) % pe_frames) * C : nullptr;
 #pragma unroll
   for (int q = 0; q < NCH; ++q) {
@@ -283,8 +287,10 @@ extern "C" int ls_groupnorm_apply(const uint16_t* x1, const uint16_t* x2, int32_
 
 template <int NCH>
 static void launch_ln(const uint16_t* x, int64_t ldx, int64_t rows, int32_t C, float eps, const float* gamma, const float* beta,
-                      const float* pe, int32_t pe_rpf, int32_t pe_frames, uint16_t* y, hipStream_t s) {
-  layernorm_kernel<NCH><<<cdiv(rows, 16), 256, 0, s>>>(x, ldx, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y);
+                      const float* pe, int32_t pe_rpf, int32_t pe_frames, uint16_t* y, hipStream_t s,
+                      float* stats = nullptr) {
+  layernorm_kernel<NCH><<<cdiv(rows, 16), 256, 0, s>>>(x, ldx, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y,
+                                                        stats);
 }
 
 extern "C" int ls_layernorm(const uint16_t* x, int64_t ldx, int64_t rows, int32_t C, float eps,
@@ -304,4 +310,21 @@ extern "C" int ls_layernorm(const uint16_t* x, int64_t ldx, int64_t rows, int32_
   else if (nch <= 12) launch_ln<12>(x, ldx, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
   else launch_ln<16>(x, ldx, rows, C, eps, gamma, beta, pe, pe_rpf, pe_frames, y, s);
   return check_launch("layernorm_kernel");
+}
+
+extern "C" int ls_row_stats(const uint16_t* x, int64_t ldx, int64_t rows, int32_t C, float eps, float* stats,
+                            void* stream) {
+  if (!x || !stats || C % 8 || C > 16 * 8 * 16 || rows <= 0 || ldx < C || ldx % 8)
+    return fail(LS_ERR_INVALID, "ls_row_stats: bad arguments (C % 8 == 0, C <= 2048, ldx >= C, ldx % 8 == 0)");
+  hipStream_t s = (hipStream_t)stream;
+  const int nch = cdiv(C / 8, 16);
+  if (nch <= 1) launch_ln<1>(x, ldx, rows, C, eps, nullptr, nullptr, nullptr, 1, 1, nullptr, s, stats);
+  else if (nch <= 2) launch_ln<2>(x, ldx, rows, C, eps, nullptr, nullptr, nullptr, 1, 1, nullptr, s, stats);
+  else if (nch <= 3) launch_ln<3>(x, ldx, rows, C, eps, nullptr, nullptr, nullptr, 1, 1, nullptr, s, stats);
+  else if (nch <= 5) launch_ln<5>(x, ldx, rows, C, eps, nullptr, nullptr, nullptr, 1, 1, nullptr, s, stats);
+  else if (nch <= 8) launch_ln<8>(x, ldx, rows, C, eps, nullptr, nullptr, nullptr, 1, 1, nullptr, s, stats);
+  else if (nch <= 10) launch_ln<10>(x, ldx, rows, C, eps, nullptr, nullptr, nullptr, 1, 1, nullptr, s, stats);
+  else if (nch <= 12) launch_ln<12>(x, ldx, rows, C, eps, nullptr, nullptr, nullptr, 1, 1, nullptr, s, stats);
+  else launch_ln<16>(x, ldx, rows, C, eps, nullptr, nullptr, nullptr, 1, 1, nullptr, s, stats);
+  return check_launch("layernorm_kernel(stats)");
 }

@@ -52,6 +52,8 @@ class Packed:
         self.N, self.K = w.shape
         self.n_out = n_out
         self.geglu = geglu
+        self.colsum = None  # set for LayerNorm-folded weights (unet._Dev.packed_ln)
+        self.pe_rows = None  # W pe table for a folded LayerNorm + positional encoding
 
 
 def _ld(t):
@@ -68,9 +70,10 @@ def _ld(t):
 
 
 def conv(x, pw: Packed, *, x2=None, aff=None, stride=1, pad=None, upsample=False, out_hw=None, rowvec=None,
-         res=None, out_scale=1.0, act=ACT_NONE, out=None, out_f32=False, split_k=0):
+         res=None, out_scale=1.0, act=ACT_NONE, out=None, out_f32=False, split_k=0, ln_stats=None):
     """Fused conv/linear.  x (n, H, W, C1) [+ x2 (n, H, W, C2)] -> (n, Ho, Wo, n_out).
-    aff = (scale[S][C], shift[S][C], imgs_per_sample, silu); rowvec = (t[S][ld], rows_per_vec, ld)."""
+    aff = (scale[S][C], shift[S][C], imgs_per_sample, silu); rowvec = (t[S][ld], rows_per_vec, ld[, mod]);
+    ln_stats = (mean, rstd) rows from row_stats(): LayerNorm folded into pw (pw.colsum)."""
     lib = _lib.load()
     n, H, W, C1 = x.shape
     C2 = x2.shape[3] if x2 is not None else 0
@@ -100,6 +103,10 @@ def conv(x, pw: Packed, *, x2=None, aff=None, stride=1, pad=None, upsample=False
     d.bias = _p(pw.bias)
     if rowvec is not None:
         d.rowvec, d.rows_per_vec, d.rowvec_ld = _p(rowvec[0]), rowvec[1], rowvec[2]
+        d.rowvec_mod = rowvec[3] if len(rowvec) > 3 else 0
+    if ln_stats is not None:
+        assert pw.colsum is not None, "ln_stats needs LayerNorm-folded weights"
+        d.ln_rowstats, d.ln_colsum = _p(ln_stats), _p(pw.colsum)
     if res is not None:
         d.res, d.ldr = _p(res), (_ld(res) if res.dim() == 4 else res.stride(-2))
     d.out_scale = out_scale
@@ -151,6 +158,16 @@ def group_norm_apply(x, scale, shift, n_samples, silu, x2=None):
 
 def affine_act(x, scale, shift, n_samples, silu):
     return group_norm_apply(x, scale, shift, n_samples, silu)
+
+
+def row_stats(x2d, eps=1e-5):
+    """(mean, rstd) fp32 per row of x2d (rows, C) (row-strided views allowed)."""
+    lib = _lib.load()
+    rows, C_ = x2d.shape
+    assert x2d.stride(1) == 1
+    st = torch.empty((rows, 2), dtype=torch.float32, device=x2d.device)
+    check(lib.ls_row_stats(_p(x2d), x2d.stride(0), rows, C_, eps, _p(st), _stream()), "ls_row_stats")
+    return st
 
 
 def layer_norm(x2d, gamma, beta, eps=1e-5, pe=None, pe_rows_per_frame=1, pe_frames=1):

@@ -9,16 +9,16 @@ HIP C-ABI library (latentsync_amd/ops.py -> libls_hip.so) on NHWC bf16
 activations with frames folded into the image index:
 
   ResnetBlock3D (resnet.py:182-223)
-      GN5D stats -> conv1 3x3 [GN-apply+SiLU prologue, bias + temb epilogue]
-      GN5D stats -> conv2 3x3 [GN-apply+SiLU prologue, bias + shortcut residual]
+      GN5D stats -> GN-apply+SiLU -> conv1 3x3 [bias + temb epilogue]
+      GN5D stats -> GN-apply+SiLU -> conv2 3x3 [bias + shortcut residual]
       the up-block torch.cat (unet_blocks.py:624,745) is fused into the gathers.
   Transformer3DModel (attention.py:82-124) + BasicTransformerBlock (:174-199)
-      GN4D stats -> proj_in 1x1 [GN prologue] -> LN -> fused q|k|v GEMM ->
+      GN4D stats -> GN-apply -> proj_in 1x1 -> LN -> fused q|k|v GEMM ->
       flash attention -> out-proj [bias + residual] -> LN -> q GEMM, audio k|v
       GEMM -> attention (Nk = 50) -> out-proj -> LN -> GEGLU GEMM (fused
       h * gelu(g) epilogue) -> FF2 [bias + residual] -> proj_out [+ residual]
   VanillaTemporalModule (motion_module.py:39-313)
-      GN4D -> proj_in [GN prologue] -> 2 x (LN + pos-enc -> q|k|v -> temporal
+      GN4D -> GN-apply -> proj_in -> 2 x (LN + pos-enc -> q|k|v -> temporal
       attention over frames via strided views -> out-proj) -> GEGLU FF -> proj_out
 """
 import math
@@ -98,6 +98,20 @@ class _Dev:
         return ops.Packed(wp.to(torch.bfloat16).to(self.device).contiguous(),
                           None if bp is None else bp.to(self.device).contiguous(), cin, ksize, n_out, geglu)
 
+    def packed_ln(self, w, b, ln, geglu=False, pe=None):
+        """nn.LayerNorm(gamma, beta) followed by linear(w, b), folded for the GEMM
+        epilogue (ls_conv_desc.ln_rowstats): Wp = W * gamma, bias = b + W beta,
+        colsum = row sums of the packed bf16 Wp; with a positional encoding added
+        after the norm (motion_module.py:267), pe_rows = pe W^T (rowvec table)."""
+        gamma, beta = (t.detach().float().cpu() for t in ln)
+        w = w.float().cpu()
+        b = (b.float().cpu() if b is not None else torch.zeros(w.shape[0])) + w @ beta
+        pk = self.packed(None, w=w * gamma[None, :], b=b, geglu=geglu)
+        pk.colsum = pk.w.float().sum(1).contiguous()
+        if pe is not None:
+            pk.pe_rows = (pe.float().cpu() @ w.T).to(self.device).contiguous()
+        return pk
+
 
 class _Resnet:
     def __init__(self, dv, p, cin, cout, groups, eps, out_scale, temb_slot):
@@ -132,17 +146,16 @@ class _Transformer:
         self.proj_out = dv.packed(p + ".proj_out.weight", p + ".proj_out.bias")
         b = p + ".transformer_blocks.0"
         sd = dv.sd
-        self.ln1 = (dv.f32(b + ".norm1.weight"), dv.f32(b + ".norm1.bias"))
-        self.qkv1 = dv.packed(None, w=torch.cat([sd[f"{b}.attn1.to_{n}.weight"] for n in "qkv"], 0))
+        ln = lambda k: (sd[k + ".weight"], sd[k + ".bias"])
+        self.qkv1 = dv.packed_ln(torch.cat([sd[f"{b}.attn1.to_{n}.weight"] for n in "qkv"], 0), None, ln(b + ".norm1"))
         self.o1 = dv.packed(b + ".attn1.to_out.0.weight", b + ".attn1.to_out.0.bias")
         self.has_audio = audio and (b + ".attn2.to_q.weight") in sd
         if self.has_audio:
-            self.ln2 = (dv.f32(b + ".norm2.weight"), dv.f32(b + ".norm2.bias"))
-            self.q2 = dv.packed(b + ".attn2.to_q.weight")
+            self.q2 = dv.packed_ln(sd[b + ".attn2.to_q.weight"], None, ln(b + ".norm2"))
             self.kv2 = dv.packed(None, w=torch.cat([sd[b + ".attn2.to_k.weight"], sd[b + ".attn2.to_v.weight"]], 0))
             self.o2 = dv.packed(b + ".attn2.to_out.0.weight", b + ".attn2.to_out.0.bias")
-        self.ln3 = (dv.f32(b + ".norm3.weight"), dv.f32(b + ".norm3.bias"))
-        self.ff1 = dv.packed(b + ".ff.net.0.proj.weight", b + ".ff.net.0.proj.bias", geglu=True)
+        self.ff1 = dv.packed_ln(sd[b + ".ff.net.0.proj.weight"], sd[b + ".ff.net.0.proj.bias"], ln(b + ".norm3"),
+                                geglu=True)
         self.ff2 = dv.packed(b + ".ff.net.2.weight", b + ".ff.net.2.bias")
 
     def __call__(self, x, audio_rows, n_audio_tok):
@@ -151,10 +164,10 @@ class _Transformer:
         rows = n * HW
         d = C // self.heads
         sc = ops.group_norm(x, self.groups, 1e-6, *self.norm, n)
-        h = ops.conv(x, self.proj_in, aff=(sc[0], sc[1], 1, False)).view(rows, C)
-        # self attention
-        t = ops.layer_norm(h, *self.ln1)
-        qkv = ops.linear(t, self.qkv1)
+        # GN affine materialised (HBM-bound, 2 B/elem each way) so proj_in runs on the DMA GEMM
+        h = ops.conv(ops.group_norm_apply(x, sc[0], sc[1], n, False), self.proj_in).view(rows, C)
+        # self attention (norm1 folded into the q|k|v GEMM)
+        qkv = ops.linear(h, self.qkv1, ln_stats=ops.row_stats(h))
         o = torch.empty((rows, C), dtype=torch.bfloat16, device=x.device)
         ops.attention(qkv, qkv[:, C:], qkv[:, 2 * C:], o, batch=n, z2=1, heads=self.heads, nq=HW, nk=HW, head_dim=d,
                       qs=(HW * 3 * C, 0, 3 * C, d), ks=(HW * 3 * C, 0, 3 * C, d), vs=(HW * 3 * C, 0, 3 * C, d),
@@ -162,17 +175,15 @@ class _Transformer:
         h = ops.linear(o, self.o1, res=h)
         # audio cross attention
         if self.has_audio and audio_rows is not None:
-            t = ops.layer_norm(h, *self.ln2)
-            q = ops.linear(t, self.q2)
+            q = ops.linear(h, self.q2, ln_stats=ops.row_stats(h))
             kv = ops.linear(audio_rows, self.kv2)
             L = n_audio_tok
             ops.attention(q, kv, kv[:, C:], o, batch=n, z2=1, heads=self.heads, nq=HW, nk=L, head_dim=d,
                           qs=(HW * C, 0, C, d), ks=(L * 2 * C, 0, 2 * C, d), vs=(L * 2 * C, 0, 2 * C, d),
                           os_=(HW * C, 0, C, d))
             h = ops.linear(o, self.o2, res=h)
-        # GEGLU feed-forward
-        t = ops.layer_norm(h, *self.ln3)
-        g = ops.linear(t, self.ff1, act=ops.ACT_GEGLU)
+        # GEGLU feed-forward (norm3 folded)
+        g = ops.linear(h, self.ff1, act=ops.ACT_GEGLU, ln_stats=ops.row_stats(h))
         h = ops.linear(g, self.ff2, res=h)
         return ops.conv(h.view(n, H, W, C), self.proj_out, res=x)
 
@@ -198,12 +209,12 @@ class _Motion:
             else:
                 pe = None
             self.attn.append(dict(
-                ln=(dv.f32(f"{b}.norms.{i}.weight"), dv.f32(f"{b}.norms.{i}.bias")),
-                qkv=dv.packed(None, w=torch.cat([sd[f"{a}.to_{n}.weight"] for n in "qkv"], 0)),
-                o=dv.packed(a + ".to_out.0.weight", a + ".to_out.0.bias"), pe=pe))
+                qkv=dv.packed_ln(torch.cat([sd[f"{a}.to_{n}.weight"] for n in "qkv"], 0), None,
+                                 (sd[f"{b}.norms.{i}.weight"], sd[f"{b}.norms.{i}.bias"]), pe=pe),
+                o=dv.packed(a + ".to_out.0.weight", a + ".to_out.0.bias")))
             i += 1
-        self.ffn = (dv.f32(b + ".ff_norm.weight"), dv.f32(b + ".ff_norm.bias"))
-        self.ff1 = dv.packed(b + ".ff.net.0.proj.weight", b + ".ff.net.0.proj.bias", geglu=True)
+        self.ff1 = dv.packed_ln(sd[b + ".ff.net.0.proj.weight"], sd[b + ".ff.net.0.proj.bias"],
+                                (sd[b + ".ff_norm.weight"], sd[b + ".ff_norm.bias"]), geglu=True)
         self.ff2 = dv.packed(b + ".ff.net.2.weight", b + ".ff.net.2.bias")
 
     def __call__(self, x, B):
@@ -213,18 +224,19 @@ class _Motion:
         rows = n * S
         d = C // self.heads
         sc = ops.group_norm(x, self.groups, 1e-6, *self.norm, n)
-        h = ops.conv(x, self.proj_in, aff=(sc[0], sc[1], 1, False)).view(rows, C)
+        # GN affine materialised (HBM-bound, 2 B/elem each way) so proj_in runs on the DMA GEMM
+        h = ops.conv(ops.group_norm_apply(x, sc[0], sc[1], n, False), self.proj_in).view(rows, C)
         o = torch.empty((rows, C), dtype=torch.bfloat16, device=x.device)
         for a in self.attn:
-            t = ops.layer_norm(h, *a["ln"], pe=a["pe"], pe_rows_per_frame=S, pe_frames=F)
-            qkv = ops.linear(t, a["qkv"])
+            pk = a["qkv"]  # LN (+ positional encoding, as the W pe row table) folded in
+            rv = (pk.pe_rows, S, pk.pe_rows.shape[1], F) if pk.pe_rows is not None else None
+            qkv = ops.linear(h, pk, ln_stats=ops.row_stats(h), rowvec=rv)
             # "(b f) s c -> (b s) f c": batch (b, s), sequence f
             st = (F * S * 3 * C, 3 * C, S * 3 * C, d)
             ops.attention(qkv, qkv[:, C:], qkv[:, 2 * C:], o, batch=B * S, z2=S, heads=self.heads, nq=F, nk=F,
                           head_dim=d, qs=st, ks=st, vs=st, os_=(F * S * C, C, S * C, d))
             h = ops.linear(o, a["o"], res=h)
-        t = ops.layer_norm(h, *self.ffn)
-        g = ops.linear(t, self.ff1, act=ops.ACT_GEGLU)
+        g = ops.linear(h, self.ff1, act=ops.ACT_GEGLU, ln_stats=ops.row_stats(h))
         h = ops.linear(g, self.ff2, res=h)
         return ops.conv(h.view(n, H, W, C), self.proj_out, res=x)
 

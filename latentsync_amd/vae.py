@@ -65,7 +65,7 @@ class _Attn:
         n, H, W, C = x.shape
         N = H * W
         s = ops.group_norm(x, 32, 1e-6, *self.gn, n)
-        qkv = ops.conv(x, self.qkv, aff=(s[0], s[1], 1, False)).view(n * N, 3 * C)
+        qkv = ops.conv(ops.group_norm_apply(x, s[0], s[1], n, False), self.qkv).view(n * N, 3 * C)
         o = torch.empty((n * N, C), dtype=torch.bfloat16, device=x.device)
         st = (N * 3 * C, 0, 3 * C, C)
         ops.attention(qkv, qkv[:, C:], qkv[:, 2 * C:], o, batch=n, z2=1, heads=1, nq=N, nk=N, head_dim=C, qs=st,

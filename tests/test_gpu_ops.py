@@ -291,3 +291,33 @@ def test_linear_strided_views(gpu):
     assert rel_err(Xc[:, 2], ref) < 1e-2
     ln = ops.layer_norm(X[:, 1], torch.ones(C, device=DEV), torch.zeros(C, device=DEV))
     assert rel_err(ln.float().cpu(), F.layer_norm(Xc[:, 1], (C,))) < 1e-2
+
+
+@pytest.mark.parametrize("geglu,pe", [(False, False), (True, False), (False, True)])
+def test_layernorm_folded_linear(gpu, geglu, pe):
+    """LayerNorm -> linear folded into the GEMM epilogue (ls_row_stats +
+    ln_rowstats/ln_colsum, + W pe row table with modulo) vs F.layer_norm then
+    linear in fp32.  Rows carry a large mean to exercise the (acc - mean*colsum)
+    cancellation.  Tolerance 1e-2."""
+    from latentsync_amd.unet import _Dev
+    M, C, N, S, Fr = 512, 320, (1280 if geglu else 960), 16, 8
+    x = bf(rnd(M, C, seed=80) * 2 + 3)
+    gamma, beta = 1 + 0.1 * rnd(C, seed=81), 0.1 * rnd(C, seed=82)
+    w = rnd(N, C, seed=83, scale=1 / math.sqrt(C))
+    b = rnd(N, seed=84, scale=0.1) if geglu else None
+    pe_t = rnd(24, C, seed=85) if pe else None
+    t = F.layer_norm(x, (C,), gamma, beta, 1e-5)
+    if pe:
+        t = t + pe_t[(torch.arange(M) // S) % Fr]
+    y_ref = t @ w.T + (b if b is not None else 0)
+    pk = _Dev({}, DEV).packed_ln(w, b, (gamma, beta), geglu=geglu, pe=pe_t)
+    xd = x.to(torch.bfloat16).to(DEV)
+    st = ops.row_stats(xd)
+    rv = (pk.pe_rows, S, pk.pe_rows.shape[1], Fr) if pe else None
+    if geglu:
+        h, g = y_ref.chunk(2, -1)
+        y_ref = h * F.gelu(g)
+        y = ops.linear(xd, pk, act=ops.ACT_GEGLU, ln_stats=st)
+    else:
+        y = ops.linear(xd, pk, ln_stats=st, rowvec=rv)
+    assert rel_err(y.float().cpu(), y_ref) < 1e-2
