@@ -652,6 +652,171 @@ __global__ void __launch_bounds__(512) conv_gemm_big_kernel(ConvArgs a) {
   store_tile<BM, BN, WM, WN>(a, acc, (float*)lds, m0, n0, z);
 }
 
+// 256 x 256 x 64 tile, 8 waves (2 M x 4 N, 128 x 64 per wave), phased schedule
+// (after the guide's 8-phase template): each K-tile runs as 4 phases, one per
+// 64 x 32 quadrant of the wave tile (16 MFMAs).  A phase issues the fragment
+// reads it needs (A quadrant rows and/or B quadrant cols), ONE half-tile of
+// operand DMA (2 glds per thread; half-tiles A0 A1 B0 B1 = 128 rows x 64 k)
+// six half-tiles ahead, barrier, MFMAs at raised priority, barrier.  The DMA
+// for tile t+1 is retired by a counted vmcnt(4) in phase 3 of tile t, so
+// operand loads span barriers and never drain in the main loop.
+template <int KS, bool TAPU>
+__global__ void __launch_bounds__(512) conv_gemm_p8_kernel(ConvArgs a) {
+  constexpr int BM = 256, BN = 256, BK = 64, CPR = 8;
+  constexpr int HALF = 128 * CPR;         // uint4 per half-tile (16 KB)
+  constexpr int BUF = 4 * HALF;           // A0 A1 B0 B1
+  constexpr int D = 6;                    // half-tiles of DMA in flight
+  extern __shared__ __attribute__((aligned(16))) uint4 lds_dyn[];
+  uint4* lds = lds_dyn;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int nt = a.ntm * a.ntn;
+  int bid = xcd_remap(blockIdx.x, nt * a.split);
+  const int z = bid / nt;
+  bid -= z * nt;
+  const int tm = bid / a.ntn, tn = bid - tm * a.ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kt0 = z * a.kt_per_split;
+  const int nk = min(a.ktiles, kt0 + a.kt_per_split) - kt0;
+  const int nhalf = 4 * nk;
+
+  // per-thread DMA geometry: instruction i (0, 1) of each half covers rows (wid*2+i)*8 + lane/8
+  int arow[4], ach[4], brow[4], bch[4];
+  RowGeo geo[4];
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = (wid * 2 + i) * 64 + lane;
+      const int row = q / CPR, pc = q % CPR;
+      const int lc = swz_bk<BK>(row, pc) - row * CPR;
+      const int p = hh * 2 + i;
+      arow[p] = m0 + hh * 128 + row;
+      ach[p] = lc;
+      brow[p] = n0 + hh * 128 + row;
+      bch[p] = lc;
+      if (KS == 3) {
+        const int m = arow[p];
+        const int hw = a.Ho * a.Wo;
+        const int n = m / hw, r = m - n * hw;
+        const int yo = r / a.Wo, xo = r - yo * a.Wo;
+        geo[p].pb = n * a.H * a.W;
+        geo[p].yb = (m < a.M) ? (a.upsample ? yo - a.pad : yo * a.stride - a.pad) : -(1 << 28);
+        geo[p].xb = a.upsample ? xo - a.pad : xo * a.stride - a.pad;
+      } else {
+        geo[p].pb = 0; geo[p].yb = 0; geo[p].xb = 0;
+      }
+    }
+  // issue half-tile s (tile s/4, half s%4: A0 A1 B0 B1) into its buffer
+  auto issue_half = [&](int s) {
+    if (s >= nhalf) return;
+    const int t = s >> 2, h = s & 3;
+    const int kt = kt0 + t;
+    uint4* dst = lds + (t & 1) * BUF + h * HALF + wid * 2 * 64;
+    if (h < 2) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int p = (h & 1) * 2 + i;
+        glds16(a_src<KS, TAPU, BK>(a, kt, ach[p], arow[p], geo[p]), dst + i * 64);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int p = (h & 1) * 2 + i;
+        const void* src = brow[p] < a.N ? (const void*)(a.w + (long)brow[p] * a.K + kt * BK + bch[p] * 8)
+                                        : (const void*)ls_zero_page;
+        glds16(src, dst + i * 64);
+      }
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // prologue: half-tiles 0 .. D-1 in flight, tile 0 landed
+#pragma unroll
+  for (int s = 0; s < D; ++s) issue_half(s);
+  if (nk > 1) wait_vm<4>(); else wait_vm<0>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  // ping-pong: the two wave rows (one wave of each per SIMD) run one barrier
+  // apart, so one wave's MFMA section overlaps the other's load section
+  if (wr == 1) __builtin_amdgcn_s_barrier();
+  bf16x8 af[2][4], b0[2][2], b1[2][2];
+  const int arow_w = wr * 128;            // this wave's rows inside the A tile (= its A half)
+  const int bh = wc >> 1, bcol = (wc & 1) * 64;  // B half + column offset inside it
+  for (int t = 0; t < nk; ++t) {
+    const uint4* buf = lds + (t & 1) * BUF;
+    const uint4* Ah = buf + wr * HALF;
+    const uint4* Bh = buf + (2 + bh) * HALF;
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      const int qm = (ph == 0 || ph == 1) ? 0 : 1;
+      const int qn = (ph == 0 || ph == 3) ? 0 : 1;
+      // fragment reads this phase needs
+      if (ph == 0 || ph == 3) {
+        if (ph == 0) {
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              b0[ks][j] = __builtin_bit_cast(
+                  bf16x8, Bh[swz_bk<BK>(bcol + j * 16 + (lane & 15), ks * 4 + (lane >> 4))]);
+        }
+      } else if (ph == 1) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            b1[ks][j] = __builtin_bit_cast(
+                bf16x8, Bh[swz_bk<BK>(bcol + 32 + j * 16 + (lane & 15), ks * 4 + (lane >> 4))]);
+      }
+      if (ph == 0 || ph == 2) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            af[ks][i] = __builtin_bit_cast(
+                bf16x8, Ah[swz_bk<BK>(qm * 64 + i * 16 + (lane & 15), ks * 4 + (lane >> 4))]);
+      }
+      (void)arow_w;
+      // one half-tile of DMA, D ahead
+      issue_half(4 * t + ph + D);
+      if (ph == 3) {  // retire tile t+1 (issued up to 4t+9 now; t+1 ends at 4t+7)
+        if (4 * t + 3 + D < nhalf) wait_vm<4>();
+        else wait_vm<0>();
+      }
+      // this phase's fragment reads retire before the barrier: a half-tile may be
+      // re-staged by the other wave row right after it
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const bf16x8 bv = qn == 0 ? b0[ks][j] : b1[ks][j];
+            acc[qm * 4 + i][qn * 2 + j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bv, acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+          }
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the rows before the LDS is reused
+  asm volatile("" ::: "memory");
+  store_tile<BM, BN, 2, 4>(a, acc, (float*)lds, m0, n0, z);
+}
+
 // split-K reduction + epilogue: one thread per 8 output columns
 __global__ void splitk_reduce_kernel(ConvArgs a) {
   const bool geglu = a.act == LS_ACT_GEGLU;
@@ -698,14 +863,16 @@ struct TileCfg { int bm, bn, split; };
 
 // Tile + split-K choice by a small cost model: time ~ max(1, blocks / CUs) x
 // per-block MFMA work / relative efficiency of the tile, + split-K slab traffic.
-static TileCfg pick_tile(long M, int N, int ktiles, bool allow_split) {
+static TileCfg pick_tile(long M, int N, int ktiles, bool allow_split, bool big_ok) {
   struct Cand { int bm, bn; double eff; };
-  const Cand cands[] = {{128, 128, 1.0}, {128, 64, 0.72}, {64, 64, 0.42}, {128, 32, 0.36}};
+  // eff = relative MFMA throughput of the tile (measured, scripts/gemm_bench.py)
+  const Cand cands[] = {{128, 128, 1.0}, {128, 64, 0.72}, {64, 64, 0.42}, {128, 32, 0.36}, {256, 256, 1.12}};
   TileCfg best{128, 128, 1};
   double best_t = 1e300;
   for (const Cand& c : cands) {
     if (c.bn == 32 && N > 32) continue;
     if (N <= 32 && c.bn != 32) continue;
+    if (c.bm == 256 && (!big_ok || (N % 256 != 0 && N < 1920))) continue;
     const long tiles = (long)cdiv(M, c.bm) * cdiv(N, c.bn);
     for (int split = 1; split <= 16; split *= 2) {
       if (split > 1 && (!allow_split || ktiles / split < 4)) break;
@@ -750,6 +917,18 @@ static void launch_big1(const ConvArgs& a, int grid, hipStream_t s) {
     attr = true;
   }
   conv_gemm_big_kernel<BN, KS, TAPU><<<grid, 512, shm, s>>>(a);
+}
+
+template <int KS, bool TAPU>
+static void launch_p8_1(const ConvArgs& a, int grid, hipStream_t s) {
+  const size_t shm = std::max<size_t>((size_t)2 * 4 * 128 * 8 * 16, (size_t)128 * (256 + 4) * 4);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)conv_gemm_p8_kernel<KS, TAPU>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)shm);
+    attr = true;
+  }
+  conv_gemm_p8_kernel<KS, TAPU><<<grid, 512, shm, s>>>(a);
 }
 
 template <int BN>
@@ -804,12 +983,14 @@ static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split
   a.y = d->y; a.ldy = d->ldy; a.y_f32 = d->y_f32;
   a.ablate = g_ablate;
   a.ktiles = d->K / 64;
-  t = pick_tile(M, d->N, a.ktiles, d->split_k <= 0 && d->workspace != nullptr);
+  t = pick_tile(M, d->N, a.ktiles, d->split_k <= 0 && d->workspace != nullptr,
+                !d->aff_scale && !g_force_regstage && (d->ksize == 1 || Cin % 64 == 0));
   if (g_force_tile) {
-    static const int tb[7][2] = {{0, 0}, {128, 128}, {128, 64}, {64, 64}, {128, 32}, {256, 256}, {256, 128}};
+    static const int tb[8][2] = {{0, 0}, {128, 128}, {128, 64}, {64, 64}, {128, 32}, {256, 256}, {256, 128},
+                                 {257, 256}};
     t.bm = tb[g_force_tile][0]; t.bn = tb[g_force_tile][1]; t.split = g_force_split ? g_force_split : 1;
   }
-  a.ntm = cdiv(M, t.bm); a.ntn = cdiv(d->N, t.bn);
+  a.ntm = cdiv(M, t.bm == 257 ? 256 : t.bm); a.ntn = cdiv(d->N, t.bn);  // 257 = phased 256x256 kernel
   split = d->split_k > 0 ? d->split_k : t.split;
   split = std::min(split, a.ktiles);
   a.kt_per_split = cdiv(a.ktiles, split);
@@ -826,7 +1007,7 @@ using namespace ls;
 extern "C" int ls_set_tuning(int32_t key, int32_t value) {
   switch (key) {
     case 1: g_force_regstage = value != 0; return LS_OK;
-    case 2: if (value < 0 || value > 6) return fail(LS_ERR_INVALID, "tile id 0..6"); g_force_tile = value; return LS_OK;
+    case 2: if (value < 0 || value > 7) return fail(LS_ERR_INVALID, "tile id 0..7"); g_force_tile = value; return LS_OK;
     case 3: g_force_split = value; return LS_OK;
     case 4: g_ablate = value; return LS_OK;
     case 5: if (value != 32 && value != 64) return fail(LS_ERR_INVALID, "BK 32 or 64"); g_bk = value; return LS_OK;
@@ -860,7 +1041,10 @@ extern "C" int ls_conv2d(const ls_conv_desc* d, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const bool tapu = (d->ksize == 3) && (a.Cin % 64 == 0);
   const int grid = a.ntm * a.ntn * a.split;
-  if (t.bm == 256 && !a.aff_scale && !g_force_regstage) {
+  if (t.bm == 257 && !a.aff_scale && !g_force_regstage && (d->ksize == 1 || tapu)) {  // phased 256x256
+    if (d->ksize == 1) launch_p8_1<1, false>(a, grid, s);
+    else launch_p8_1<3, true>(a, grid, s);
+  } else if (t.bm == 256 && !a.aff_scale && !g_force_regstage) {
     if (t.bn == 256) launch_big<256>(a, d->ksize, tapu, grid, s);
     else launch_big<128>(a, d->ksize, tapu, grid, s);
   } else if (t.bm == 128 && t.bn == 128) launch_cfg<128, 128, 2, 2>(a, d->ksize, tapu, grid, s);

@@ -28,14 +28,24 @@ def run(tag, reps=20, scale=1):
         w = torch.randn(cout, cin, ks, ks) / (cin * ks * ks) ** 0.5
         pw = ops.Packed(pack_weight(w).to(torch.bfloat16).cuda(), torch.zeros(cout, device="cuda"), cin, ks, cout,
                         geglu=act == 1)
-        f = lambda: ops.conv(x, pw, act=act)
-        for _ in range(3):
-            f()
+        out = ops.conv(x, pw, act=act)
+        torch.cuda.synchronize()
+        # graph of 10 launches: GPU time without host submission gaps
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(10):
+                    ops.conv(x, pw, act=act, out=out)
+        torch.cuda.current_stream().wait_stream(s)
+        g.replay()
+        torch.cuda.synchronize()
         ts = []
         for _ in range(reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(); f(); e1.record(); torch.cuda.synchronize()
-            ts.append(e0.elapsed_time(e1))
+            e0.record(); g.replay(); e1.record(); torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) / 10)
         t = statistics.median(ts)
         fl = 2.0 * n * H * H * cout * cin * ks * ks
         tot_f += fl; tot_t += t
