@@ -173,6 +173,218 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
   }
 }
 
+// Long-sequence variant (nk > 32): every wave owns 32 queries (two Q fragments
+// share each K/V fragment read), 64-key tiles double-buffered in LDS with the
+// next tile's global loads issued into registers before the current tile's
+// MFMAs (one barrier per tile), QK^T over KC 32-wide d chunks but PV over only
+// ND = ceil(D/16) output fragments (d = 40 pays 48, not 64), and the softmax
+// exponent formed with one FMA (s * scale*log2e - m).
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+template <int KC, int ND>
+__global__ void __launch_bounds__(256) attn2_kernel(AttnArgs a) {
+  constexpr int DP = KC * 32;
+  constexpr int KT = 64;
+  constexpr int PITCH = DP + 8;
+  constexpr int TILE = KT * PITCH;          // elements per K (or V) tile
+  constexpr int CPR = ND * 2;               // max 16-B chunks per row actually loaded (D <= 16 ND)
+  constexpr int LPT = (KT * CPR + 255) / 256;  // chunks per thread per operand
+  extern __shared__ __attribute__((aligned(16))) u16 sm[];  // [2][K, V]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int h = blockIdx.y;
+  const int b = blockIdx.z;
+  const long b1 = b / a.z2, b2 = b - b1 * a.z2;
+  const u16* qb = a.q + b1 * a.q_sb1 + b2 * a.q_sb2 + (long)h * a.q_sh;
+  const u16* kb = a.k + b1 * a.k_sb1 + b2 * a.k_sb2 + (long)h * a.k_sh;
+  const u16* vb = a.v + b1 * a.v_sb1 + b2 * a.v_sb2 + (long)h * a.v_sh;
+  u16* ob = a.o + b1 * a.o_sb1 + b2 * a.o_sb2 + (long)h * a.o_sh;
+  const int q0 = (blockIdx.x * 4 + wid) * 32;
+  const int lq = lane & 15, lg = lane >> 4;
+  const int cpr = (a.D + 7) >> 3;           // chunks per row present in memory
+
+  // zero the d padding of both K buffers once (QK^T reads d up to DP)
+  for (int i = tid; i < 2 * KT; i += 256) {
+    u16* row = sm + (i / KT) * 2 * TILE + (i % KT) * PITCH;
+    for (int c = cpr * 8; c < DP; c += 8) *(uint4*)(row + c) = make_uint4(0, 0, 0, 0);
+  }
+
+  bf16x8 qf[2][KC];
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      const int d = kc * 32 + lg * 8;
+      const int q = q0 + g * 16 + lq;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (q < a.nq && d < a.D) v = *(const uint4*)(qb + (long)q * a.q_si + d);
+      qf[g][kc] = __builtin_bit_cast(bf16x8, v);
+    }
+
+  uint4 kr[LPT], vr[LPT];
+  auto gload = [&](int t0) {
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      const int i = tid + u * 256;
+      const int r = i / CPR, c = i - r * CPR;
+      kr[u] = make_uint4(0, 0, 0, 0);
+      vr[u] = make_uint4(0, 0, 0, 0);
+      if (i < KT * CPR && c < cpr && t0 + r < a.nk) {
+        kr[u] = *(const uint4*)(kb + (long)(t0 + r) * a.k_si + c * 8);
+        vr[u] = *(const uint4*)(vb + (long)(t0 + r) * a.v_si + c * 8);
+      }
+    }
+  };
+  auto lstore = [&](int buf) {
+    u16* Ks = sm + buf * 2 * TILE;
+    u16* Vs = Ks + TILE;
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      const int i = tid + u * 256;
+      const int r = i / CPR, c = i - r * CPR;
+      if (i < KT * CPR && c < cpr) {
+        *(uint4*)(Ks + r * PITCH + c * 8) = kr[u];
+        *(uint4*)(Vs + r * PITCH + c * 8) = vr[u];
+      }
+    }
+  };
+
+  f32x4 oacc[2][ND];
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int i = 0; i < ND; ++i) oacc[g][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+  const float c2 = a.scale_log2;
+
+  gload(0);
+  __syncthreads();  // padding zeroed
+  lstore(0);
+  const int ntile = (a.nk + KT - 1) / KT;
+  for (int t = 0; t < ntile; ++t) {
+    const int t0 = t * KT;
+    __syncthreads();  // tile t visible; buffer t^1 free
+    if (t + 1 < ntile) gload(t0 + KT);
+    const u16* Ks = sm + (t & 1) * 2 * TILE;
+    const u16* Vs = Ks + TILE;
+    // S^T = K Q^T for both query fragments
+    f32x4 s[2][4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      s[0][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      s[1][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        const bf16x8 kf = __builtin_bit_cast(bf16x8, *(const uint4*)(Ks + (16 * f + lq) * PITCH + kc * 32 + lg * 8));
+        s[0][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[0][kc], s[0][f], 0, 0, 0);
+        s[1][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[1][kc], s[1][f], 0, 0, 0);
+      }
+    }
+    const bool full = t0 + KT <= a.nk;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      if (!full) {
+#pragma unroll
+        for (int f = 0; f < 4; ++f)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (t0 + 16 * f + 4 * lg + r >= a.nk) s[g][f][r] = -INFINITY;
+      }
+      float mt = fmaxf(fmaxf(s[g][0][0], s[g][0][1]), fmaxf(s[g][0][2], s[g][0][3]));
+#pragma unroll
+      for (int f = 1; f < 4; ++f)
+        mt = fmaxf(mt, fmaxf(fmaxf(s[g][f][0], s[g][f][1]), fmaxf(s[g][f][2], s[g][f][3])));
+      mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float mn = fmaxf(m[g], mt * c2);
+      const float alpha = exp2f(m[g] - mn);
+      m[g] = mn;
+      f2v ps = {0.f, 0.f};
+      const f2v cc = {c2, c2}, nm = {-mn, -mn};
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int r = 0; r < 4; r += 2) {
+          f2v x = {s[g][f][r], s[g][f][r + 1]};
+          x = x * cc + nm;
+          x.x = exp2f(x.x);
+          x.y = exp2f(x.y);
+          s[g][f][r] = x.x;
+          s[g][f][r + 1] = x.y;
+          ps += x;
+        }
+      l[g] = l[g] * alpha + ps.x + ps.y;
+#pragma unroll
+      for (int i = 0; i < ND; ++i) oacc[g][i] *= alpha;
+    }
+    // O^T += V^T P^T over 32-key chunks
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      bf16x8 pb[2];
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pb[g][r] = (__bf16)s[g][2 * c][r];
+          pb[g][4 + r] = (__bf16)s[g][2 * c + 1][r];
+        }
+      const int qq = lq >> 2, pp = lq & 3;
+      const u16* va = Vs + (32 * c + 4 * lg + qq) * PITCH + 4 * pp;
+      const u16* vb2 = va + 16 * PITCH;
+#pragma unroll
+      for (int nd = 0; nd < ND; ++nd) {
+        const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)(va + nd * 16));
+        const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)(vb2 + nd * 16));
+        const short __attribute__((ext_vector_type(8))) av = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const bf16x8 vf = __builtin_bit_cast(bf16x8, av);
+        oacc[0][nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[0], oacc[0][nd], 0, 0, 0);
+        oacc[1][nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[1], oacc[1][nd], 0, 0, 0);
+      }
+    }
+    if (t + 1 < ntile) lstore((t + 1) & 1);
+  }
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    float lt = l[g];
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    const float inv = 1.f / lt;
+    const int q = q0 + g * 16 + lq;
+    if (q < a.nq) {
+      u16* orow = ob + (long)q * a.o_si;
+#pragma unroll
+      for (int nd = 0; nd < ND; ++nd) {
+        const int d = nd * 16 + 4 * lg;
+        if (d + 3 < a.D) {
+          uint2 w;
+          w.x = (uint32_t)f2bf(oacc[g][nd][0] * inv) | ((uint32_t)f2bf(oacc[g][nd][1] * inv) << 16);
+          w.y = (uint32_t)f2bf(oacc[g][nd][2] * inv) | ((uint32_t)f2bf(oacc[g][nd][3] * inv) << 16);
+          *(uint2*)(orow + d) = w;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (d + r < a.D) orow[d + r] = f2bf(oacc[g][nd][r] * inv);
+        }
+      }
+    }
+  }
+}
+
+template <int KC, int ND>
+static int launch_attn2(const AttnArgs& a, int batch, int heads, hipStream_t s) {
+  const dim3 grid(cdiv(a.nq, 128), heads, batch);
+  const size_t shm = 2 * 2 * (size_t)64 * (KC * 32 + 8) * sizeof(u16);
+  if (shm > 64 * 1024) {
+    static bool attr_set = false;
+    if (!attr_set) {
+      hipFuncSetAttribute((const void*)attn2_kernel<KC, ND>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+      attr_set = true;
+    }
+  }
+  attn2_kernel<KC, ND><<<grid, 256, shm, s>>>(a);
+  return check_launch("attn2_kernel");
+}
+
 template <int DP, int NKF>
 static int launch_attn(const AttnArgs& a, int batch, int heads, hipStream_t s) {
   const int nwant = cdiv(a.nq, 16);
@@ -194,6 +406,8 @@ static int launch_attn(const AttnArgs& a, int batch, int heads, hipStream_t s) {
 
 using namespace ls;
 
+static bool g_attn_v1 = getenv("LS_ATTN_V1") != nullptr;  // A/B switch: force the 16-query kernel
+
 extern "C" int ls_attention(const ls_attn_desc* d, void* stream) {
   if (!d || !d->q || !d->k || !d->v || !d->o) return fail(LS_ERR_INVALID, "ls_attention: null pointer");
   if (d->head_dim % 2 || d->head_dim <= 0 || d->head_dim > 512 || d->nq <= 0 || d->nk <= 0 || d->batch <= 0 ||
@@ -210,6 +424,18 @@ extern "C" int ls_attention(const ls_attn_desc* d, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const bool small = d->nk <= 32;
   const int D = d->head_dim;
+  if (!small && D % 8 == 0 && D <= 160 && !g_attn_v1) {
+    // ND = ceil(D / 16) output fragments, KC = ceil(D / 32) contraction chunks
+    switch ((D + 15) / 16) {
+      case 1: case 2: return launch_attn2<1, 2>(a, d->batch, d->heads, s);
+      case 3: return launch_attn2<2, 3>(a, d->batch, d->heads, s);
+      case 4: return launch_attn2<2, 4>(a, d->batch, d->heads, s);
+      case 5: return launch_attn2<3, 5>(a, d->batch, d->heads, s);
+      case 6: return launch_attn2<3, 6>(a, d->batch, d->heads, s);
+      case 7: case 8: return launch_attn2<4, 8>(a, d->batch, d->heads, s);
+      default: return launch_attn2<5, 10>(a, d->batch, d->heads, s);
+    }
+  }
 #define LS_ATTN(DPV)                                                              \
   return small ? launch_attn<DPV, 2>(a, d->batch, d->heads, s)                    \
                : launch_attn<DPV, 4>(a, d->batch, d->heads, s);

@@ -40,9 +40,21 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
 }
 
-__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+// x * sigmoid(x) with a hardware reciprocal (1-2 ulp; outputs are bf16)
+__device__ __forceinline__ float silu(float x) { return x * __frcp_rn(1.0f + __expf(-x)); }
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// exact-erf GELU (diffusers GEGLU / whisper MLP) with a branch-free erf:
+// Abramowitz & Stegun 7.1.26 (|erf error| <= 1.5e-7; GELU abs error < 5e-7),
+// one reciprocal + one exp2 instead of ocml erff's range-split polynomial.
+__device__ __forceinline__ float gelu_erf(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __frcp_rn(fmaf(0.3275911f, z, 1.0f));
+  const float p = t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f),
+                           0.254829592f);
+  const float e = exp2f(-z * z * 1.4426950408889634f);
+  const float erfz = fmaf(-p, e, 1.0f);
+  return 0.5f * x * (1.0f + copysignf(erfz, x));
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

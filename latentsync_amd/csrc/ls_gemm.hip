@@ -817,6 +817,124 @@ __global__ void __launch_bounds__(512) conv_gemm_p8_kernel(ConvArgs a) {
   store_tile<BM, BN, 2, 4>(a, acc, (float*)lds, m0, n0, z);
 }
 
+// 256 x 256 tile, 8 waves (128 x 64 per wave), BK = 32 with a 4-stage LDS ring
+// (4 x 32 KB): the DMA runs three K-tiles ahead of the MFMAs behind a counted
+// vmcnt, one raw barrier per K-tile.  For operand streams that come from the
+// Infinity Cache / HBM rather than L2 (the 2-stage BK = 64 ring can only cover
+// one K-tile of latency).
+template <int KS, bool TAPU>
+__global__ void __launch_bounds__(512) conv_gemm_big4_kernel(ConvArgs a) {
+  constexpr int BM = 256, BN = 256, BK = 32, NST = 4, WM = 2, WN = 4;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int FM = WTM / 16, FN = WTN / 16, FH = FM / 2;
+  constexpr int CPR = BK / 8;
+  constexpr int AI = BM * CPR / 512, BI = BN * CPR / 512;  // 2 + 2 glds per thread per stage
+  constexpr int L = AI + BI;
+  constexpr int STAGE = (BM + BN) * CPR;
+  extern __shared__ __attribute__((aligned(16))) uint4 lds_dyn[];
+  uint4* lds = lds_dyn;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int nt = a.ntm * a.ntn;
+  int bid = xcd_remap(blockIdx.x, nt * a.split);
+  const int z = bid / nt;
+  bid -= z * nt;
+  const int tm = bid / a.ntn, tn = bid - tm * a.ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kps = a.kt_per_split * 2;  // 32-wide K-tiles per split
+  const int kt0 = z * kps;
+  const int kt1 = min(a.ktiles * 2, kt0 + kps);
+
+  int arow[AI], ach[AI], brow[BI], bch[BI];
+  RowGeo geo[AI];
+#pragma unroll
+  for (int p = 0; p < AI; ++p) {
+    const int q = (wid * AI + p) * 64 + lane;
+    const int row = q / CPR;
+    arow[p] = m0 + row;
+    ach[p] = swz_bk<BK>(row, q % CPR) - row * CPR;
+    if (KS == 3) {
+      const int m = m0 + row;
+      const int hw = a.Ho * a.Wo;
+      const int n = m / hw, r = m - n * hw;
+      const int yo = r / a.Wo, xo = r - yo * a.Wo;
+      geo[p].pb = n * a.H * a.W;
+      geo[p].yb = (m < a.M) ? (a.upsample ? yo - a.pad : yo * a.stride - a.pad) : -(1 << 28);
+      geo[p].xb = a.upsample ? xo - a.pad : xo * a.stride - a.pad;
+    } else {
+      geo[p].pb = 0; geo[p].yb = 0; geo[p].xb = 0;
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < BI; ++p) {
+    const int q = (wid * BI + p) * 64 + lane;
+    const int row = q / CPR;
+    brow[p] = n0 + row;
+    bch[p] = swz_bk<BK>(row, q % CPR) - row * CPR;
+  }
+  auto issue = [&](int kt, int stage) {
+    uint4* base = lds + stage * STAGE;
+#pragma unroll
+    for (int p = 0; p < AI; ++p)
+      glds16(a_src<KS, TAPU, BK>(a, kt, ach[p], arow[p], geo[p]), base + (wid * AI + p) * 64);
+#pragma unroll
+    for (int p = 0; p < BI; ++p) {
+      const void* src = brow[p] < a.N ? (const void*)(a.w + (long)brow[p] * a.K + kt * BK + bch[p] * 8)
+                                      : (const void*)ls_zero_page;
+      glds16(src, base + BM * CPR + (wid * BI + p) * 64);
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int t = 0; t < NST - 1; ++t)
+    if (kt0 + t < kt1) issue(kt0 + t, t);
+  int stage = 0;
+  for (int kt = kt0; kt < kt1; ++kt) {
+    // tile kt landed for this wave: later tiles (up to 2) may stay in flight
+    const int ahead = min(NST - 2, kt1 - 1 - kt);
+    if (ahead >= 2) wait_vm<2 * L>();
+    else if (ahead == 1) wait_vm<L>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();  // everyone's tile kt landed; stage of kt-1 free
+    asm volatile("" ::: "memory");
+    if (kt + NST - 1 < kt1) issue(kt + NST - 1, (stage + NST - 1) & (NST - 1));
+    const uint4* cur = lds + stage * STAGE;
+    const int c = lane >> 4;
+    bf16x8 bfr[FN], a0[FH], a1[FH];
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+      bfr[j] = __builtin_bit_cast(bf16x8, cur[BM * CPR + swz_bk<BK>(wn * WTN + j * 16 + (lane & 15), c)]);
+#pragma unroll
+    for (int i = 0; i < FH; ++i) a0[i] = __builtin_bit_cast(bf16x8, cur[swz_bk<BK>(wm * WTM + i * 16 + (lane & 15), c)]);
+#pragma unroll
+    for (int i = 0; i < FH; ++i)
+      a1[i] = __builtin_bit_cast(bf16x8, cur[swz_bk<BK>(wm * WTM + (FH + i) * 16 + (lane & 15), c)]);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < FH; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], bfr[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < FH; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[FH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], bfr[j], acc[FH + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    stage = (stage + 1) & (NST - 1);
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  store_tile<BM, BN, WM, WN>(a, acc, (float*)lds, m0, n0, z);
+}
+
 // split-K reduction + epilogue: one thread per 8 output columns
 __global__ void splitk_reduce_kernel(ConvArgs a) {
   const bool geglu = a.act == LS_ACT_GEGLU;
@@ -920,6 +1038,18 @@ static void launch_big1(const ConvArgs& a, int grid, hipStream_t s) {
 }
 
 template <int KS, bool TAPU>
+static void launch_big4(const ConvArgs& a, int grid, hipStream_t s) {
+  const size_t shm = std::max<size_t>((size_t)4 * (256 + 256) * 4 * 16, (size_t)128 * (256 + 4) * 4);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)conv_gemm_big4_kernel<KS, TAPU>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)shm);
+    attr = true;
+  }
+  conv_gemm_big4_kernel<KS, TAPU><<<grid, 512, shm, s>>>(a);
+}
+
+template <int KS, bool TAPU>
 static void launch_p8_1(const ConvArgs& a, int grid, hipStream_t s) {
   const size_t shm = std::max<size_t>((size_t)2 * 4 * 128 * 8 * 16, (size_t)128 * (256 + 4) * 4);
   static bool attr = false;
@@ -986,11 +1116,11 @@ static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split
   t = pick_tile(M, d->N, a.ktiles, d->split_k <= 0 && d->workspace != nullptr,
                 !d->aff_scale && !g_force_regstage && (d->ksize == 1 || Cin % 64 == 0));
   if (g_force_tile) {
-    static const int tb[8][2] = {{0, 0}, {128, 128}, {128, 64}, {64, 64}, {128, 32}, {256, 256}, {256, 128},
-                                 {257, 256}};
+    static const int tb[9][2] = {{0, 0}, {128, 128}, {128, 64}, {64, 64}, {128, 32}, {256, 256}, {256, 128},
+                                 {257, 256}, {258, 256}};
     t.bm = tb[g_force_tile][0]; t.bn = tb[g_force_tile][1]; t.split = g_force_split ? g_force_split : 1;
   }
-  a.ntm = cdiv(M, t.bm == 257 ? 256 : t.bm); a.ntn = cdiv(d->N, t.bn);  // 257 = phased 256x256 kernel
+  a.ntm = cdiv(M, t.bm > 256 ? 256 : t.bm); a.ntn = cdiv(d->N, t.bn);  // 257/258 = 256x256 kernel variants
   split = d->split_k > 0 ? d->split_k : t.split;
   split = std::min(split, a.ktiles);
   a.kt_per_split = cdiv(a.ktiles, split);
@@ -1007,7 +1137,7 @@ using namespace ls;
 extern "C" int ls_set_tuning(int32_t key, int32_t value) {
   switch (key) {
     case 1: g_force_regstage = value != 0; return LS_OK;
-    case 2: if (value < 0 || value > 7) return fail(LS_ERR_INVALID, "tile id 0..7"); g_force_tile = value; return LS_OK;
+    case 2: if (value < 0 || value > 8) return fail(LS_ERR_INVALID, "tile id 0..8"); g_force_tile = value; return LS_OK;
     case 3: g_force_split = value; return LS_OK;
     case 4: g_ablate = value; return LS_OK;
     case 5: if (value != 32 && value != 64) return fail(LS_ERR_INVALID, "BK 32 or 64"); g_bk = value; return LS_OK;
@@ -1044,6 +1174,9 @@ extern "C" int ls_conv2d(const ls_conv_desc* d, void* stream) {
   if (t.bm == 257 && !a.aff_scale && !g_force_regstage && (d->ksize == 1 || tapu)) {  // phased 256x256
     if (d->ksize == 1) launch_p8_1<1, false>(a, grid, s);
     else launch_p8_1<3, true>(a, grid, s);
+  } else if (t.bm == 258 && !a.aff_scale && !g_force_regstage && (d->ksize == 1 || tapu)) {  // 4-stage BK 32
+    if (d->ksize == 1) launch_big4<1, false>(a, grid, s);
+    else launch_big4<3, true>(a, grid, s);
   } else if (t.bm == 256 && !a.aff_scale && !g_force_regstage) {
     if (t.bn == 256) launch_big<256>(a, d->ksize, tapu, grid, s);
     else launch_big<128>(a, d->ksize, tapu, grid, s);

@@ -22,7 +22,10 @@ SHAPES = [  # (name, n_img, H, Cin, Cout, ksize, act)
 
 def run(tag, reps=20, scale=1):
     tot_f, tot_t = 0.0, 0.0
+    only = os.environ.get("GEMM_ONLY")
     for name, n, H, cin, cout, ks, act in SHAPES:
+        if only and only not in name:
+            continue
         n = n * scale
         x = torch.randn(n, H, H, cin, device="cuda").to(torch.bfloat16)
         w = torch.randn(cout, cin, ks, ks) / (cin * ks * ks) ** 0.5

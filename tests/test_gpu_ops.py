@@ -151,7 +151,8 @@ def _sdpa(q, k, v, scale=None):
 
 @pytest.mark.parametrize("n,N,Nk,heads,d", [(4, 256, 256, 8, 40), (2, 64, 64, 8, 80), (2, 16, 16, 8, 160),
                                             (3, 256, 50, 8, 40), (2, 64, 50, 8, 160), (1, 100, 100, 6, 64),
-                                            (2, 64, 64, 1, 512), (2, 1024, 1024, 1, 128), (2, 64, 64, 8, 4)])
+                                            (2, 64, 64, 1, 512), (2, 1024, 1024, 1, 128), (2, 64, 64, 8, 4),
+                                            (2, 1000, 777, 8, 40), (2, 200, 130, 8, 80)])
 def test_attention_spatial(gpu, n, N, Nk, heads, d):
     C = heads * d
     q = bf(rnd(n, N, C, seed=50))
@@ -239,7 +240,7 @@ def forced_tile():
     lib.ls_set_tuning(3, 0)
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 5, 6, 7])
+@pytest.mark.parametrize("tile", [1, 2, 3, 5, 6, 7, 8])
 @pytest.mark.parametrize("case", ["linear_res", "geglu", "conv3x3", "conv3x3_up_s2", "split2"])
 def test_gemm_tiles(gpu, forced_tile, tile, case):
     """Every tile configuration of ls_conv2d (incl. the 8-wave 256-row kernel) on
