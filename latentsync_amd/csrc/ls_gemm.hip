@@ -984,13 +984,17 @@ struct TileCfg { int bm, bn, split; };
 static TileCfg pick_tile(long M, int N, int ktiles, bool allow_split, bool big_ok) {
   struct Cand { int bm, bn; double eff; };
   // eff = relative MFMA throughput of the tile (measured, scripts/gemm_bench.py)
-  const Cand cands[] = {{128, 128, 1.0}, {128, 64, 0.72}, {64, 64, 0.42}, {128, 32, 0.36}, {256, 256, 1.12}};
+  const Cand cands[] = {{128, 128, 1.0}, {128, 160, 1.2}, {128, 64, 0.72}, {64, 64, 0.42}, {128, 32, 0.36},
+                        {256, 256, 1.35}};
   TileCfg best{128, 128, 1};
   double best_t = 1e300;
   for (const Cand& c : cands) {
     if (c.bn == 32 && N > 32) continue;
     if (N <= 32 && c.bn != 32) continue;
-    if (c.bm == 256 && (!big_ok || (N % 256 != 0 && N < 1920))) continue;
+    // 256x256 pays off on wide N (GEGLU W1, fused q|k|v at 1280 channels) or when
+    // 160 does not divide N (the VAE's 512); measured with scripts/gemm_bench.py
+    if (c.bm == 256 && (!big_ok || (N % 256 != 0 && N < 1920) || (N <= 1280 && N % 160 == 0))) continue;
+    if (c.bn == 160 && N % 160 != 0) continue;  // the UNet's widths are all multiples of 160
     const long tiles = (long)cdiv(M, c.bm) * cdiv(N, c.bn);
     for (int split = 1; split <= 16; split *= 2) {
       if (split > 1 && (!allow_split || ktiles / split < 4)) break;
@@ -1116,8 +1120,8 @@ static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split
   t = pick_tile(M, d->N, a.ktiles, d->split_k <= 0 && d->workspace != nullptr,
                 !d->aff_scale && !g_force_regstage && (d->ksize == 1 || Cin % 64 == 0));
   if (g_force_tile) {
-    static const int tb[9][2] = {{0, 0}, {128, 128}, {128, 64}, {64, 64}, {128, 32}, {256, 256}, {256, 128},
-                                 {257, 256}, {258, 256}};
+    static const int tb[10][2] = {{0, 0}, {128, 128}, {128, 64}, {64, 64}, {128, 32}, {256, 256}, {256, 128},
+                                  {257, 256}, {258, 256}, {128, 160}};
     t.bm = tb[g_force_tile][0]; t.bn = tb[g_force_tile][1]; t.split = g_force_split ? g_force_split : 1;
   }
   a.ntm = cdiv(M, t.bm > 256 ? 256 : t.bm); a.ntn = cdiv(d->N, t.bn);  // 257/258 = 256x256 kernel variants
@@ -1137,7 +1141,7 @@ using namespace ls;
 extern "C" int ls_set_tuning(int32_t key, int32_t value) {
   switch (key) {
     case 1: g_force_regstage = value != 0; return LS_OK;
-    case 2: if (value < 0 || value > 8) return fail(LS_ERR_INVALID, "tile id 0..8"); g_force_tile = value; return LS_OK;
+    case 2: if (value < 0 || value > 9) return fail(LS_ERR_INVALID, "tile id 0..9"); g_force_tile = value; return LS_OK;
     case 3: g_force_split = value; return LS_OK;
     case 4: g_ablate = value; return LS_OK;
     case 5: if (value != 32 && value != 64) return fail(LS_ERR_INVALID, "BK 32 or 64"); g_bk = value; return LS_OK;
@@ -1181,6 +1185,7 @@ extern "C" int ls_conv2d(const ls_conv_desc* d, void* stream) {
     if (t.bn == 256) launch_big<256>(a, d->ksize, tapu, grid, s);
     else launch_big<128>(a, d->ksize, tapu, grid, s);
   } else if (t.bm == 128 && t.bn == 128) launch_cfg<128, 128, 2, 2>(a, d->ksize, tapu, grid, s);
+  else if (t.bm == 128 && t.bn == 160) launch_cfg<128, 160, 2, 2>(a, d->ksize, tapu, grid, s);
   else if (t.bm == 128 && t.bn == 64) launch_cfg<128, 64, 2, 2>(a, d->ksize, tapu, grid, s);
   else if (t.bm == 128 && t.bn == 32) launch_cfg<128, 32, 4, 1>(a, d->ksize, tapu, grid, s);
   else launch_cfg<64, 64, 2, 2>(a, d->ksize, tapu, grid, s);

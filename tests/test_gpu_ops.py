@@ -240,7 +240,7 @@ def forced_tile():
     lib.ls_set_tuning(3, 0)
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 5, 6, 7, 8])
+@pytest.mark.parametrize("tile", [1, 2, 3, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("case", ["linear_res", "geglu", "conv3x3", "conv3x3_up_s2", "split2"])
 def test_gemm_tiles(gpu, forced_tile, tile, case):
     """Every tile configuration of ls_conv2d (incl. the 8-wave 256-row kernel) on
