@@ -36,10 +36,16 @@ from latentsync_amd.vae import AutoencoderKL  # noqa: E402
 
 SCHED_CFG = dict(beta_end=0.012, beta_schedule="scaled_linear", beta_start=0.00085, clip_sample=False,
                  num_train_timesteps=1000, set_alpha_to_one=False, steps_offset=1)  # configs/scheduler_config.json
-UNET_TF = 4.0505      # TF per UNet fwd, B=1, F=16, 256^2
-VAE_ENC_TF = 0.2727   # per frame
-VAE_DEC_TF = 0.6222   # per frame
+# algorithmic TFLOP: UNet fwd at B=1, F=16; VAE encode / decode per frame
+WORK_TF = {256: (4.0505, 0.2727, 0.6222), 512: (17.626, 1.1167, 2.5145)}
 PEAK_BF16_TF = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+# BASELINE.json configs this bench can run on one GPU (configs[0] is the CPU-only
+# plumbing case, configs[3] is configs[1] sharded over 8 ranks)
+PRESETS = {
+    1: dict(resolution=256, guidance=1.0, steps=20, windows=8),
+    2: dict(resolution=256, guidance=2.0, steps=50, windows=4),
+    4: dict(resolution=512, guidance=1.0, steps=20, windows=2),
+}
 
 
 def synthetic_window(F, R, h, cross_dim, seed, device):
@@ -57,66 +63,121 @@ def synthetic_window(F, R, h, cross_dim, seed, device):
     return [t.to(device) for t in (faces, audio, init, em, er)]
 
 
-def conv_probe(unet, engine, device):
-    """Live HIP-event timing of every ls_conv2d launch of one UNet forward (the
-    dominant kernel family, conv_gemm_kernel): algorithmic FLOPs 2*M*N*K_real
-    per launch / measured duration, on the stream the kernels run on."""
-    recs = []
-    orig = ops.conv
+def step_probe(engine, device):
+    """Live HIP-event timing of one denoising step (UNet fwd + CFG/DDIM), on the
+    stream the kernels run on (eager launches, same kernels as the graph):
+      * every ls_conv2d call (the dominant kernel family, conv_gemm_*: GEMM + its
+        split-K reduce when split) -- algorithmic FLOPs 2*M*N*Cin*k^2 per call;
+      * every ls_attention call (SDPA) -- 4*batch*heads*nq*nk*d FLOPs;
+      * every Transformer3DModel / motion-module block as a
+        whole: its GEMM + SDPA FLOPs over its wall time = the "UNet attention"
+        MFMA utilisation of the north star."""
+    from latentsync_amd import unet as U
+    convs, attns, blocks, conv_bytes = [], [], [], []
+    depth = [0]
+    orig_conv, orig_attn = ops.conv, ops.attention
+    orig_t, orig_m = U._Transformer.__call__, U._Motion.__call__
 
-    def timed(x, pw, **kw):
-        s = torch.cuda.current_stream()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(s)
-        y = orig(x, pw, **kw)
-        e1.record(s)
+    def ev():
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(torch.cuda.current_stream())
+        return e
+
+    def conv(x, pw, **kw):
+        e0 = ev()
+        y = orig_conv(x, pw, **kw)
+        e1 = ev()
         x2 = kw.get("x2")
         cin = x.shape[-1] + (x2.shape[-1] if x2 is not None else 0)
         M = y.shape[0] * y.shape[1] * y.shape[2]
-        nreal = pw.N
-        flops = 2.0 * M * nreal * cin * pw.ksize * pw.ksize
-        recs.append((e0, e1, flops))
+        f = 2.0 * M * pw.N * cin * pw.ksize * pw.ksize
+        # algorithmic HBM bytes: input pixels once, weights once, output (+ residual) once
+        nb = (x.numel() + (x2.numel() if x2 is not None else 0) + pw.w.numel()) * 2 + y.numel() * y.element_size()
+        if kw.get("res") is not None:
+            nb += y.numel() * 2
+        conv_bytes.append(nb)
+        convs.append((e0, e1, f))
+        if depth[0]:
+            blocks[-1][2] += f
         return y
 
-    ops.conv = timed
+    def attention(q, k, v, o, **kw):
+        e0 = ev()
+        r = orig_attn(q, k, v, o, **kw)
+        e1 = ev()
+        f = 4.0 * kw["batch"] * kw["heads"] * kw["nq"] * kw["nk"] * kw["head_dim"]
+        attns.append((e0, e1, f))
+        if depth[0]:
+            blocks[-1][2] += f
+        return r
+
+    def wrap(fn):
+        def call(self, *a, **kw):
+            blocks.append([ev(), None, 0.0])
+            depth[0] += 1
+            try:
+                return fn(self, *a, **kw)
+            finally:
+                depth[0] -= 1
+                blocks[-1][1] = ev()
+        return call
+
+    ops.conv, ops.attention = conv, attention
+    U._Transformer.__call__, U._Motion.__call__ = wrap(orig_t), wrap(orig_m)
     try:
         engine._step()
     finally:
-        ops.conv = orig
+        ops.conv, ops.attention = orig_conv, orig_attn
+        U._Transformer.__call__, U._Motion.__call__ = orig_t, orig_m
     torch.cuda.synchronize(device)
-    ms = [a.elapsed_time(b) for a, b, _ in recs]
-    fl = [f for _, _, f in recs]
-    tot_ms, tot_f = sum(ms), sum(fl)
-    return dict(launches=len(recs), total_ms=tot_ms, avg_ms=tot_ms / len(recs), tflops=tot_f / (tot_ms * 1e-3) / 1e12,
-                flops_per_launch=tot_f / len(recs))
+
+    def agg(recs):
+        ms = sum(a.elapsed_time(b) for a, b, _ in recs)
+        fl = sum(f for _, _, f in recs)
+        return dict(launches=len(recs), total_ms=ms, avg_ms=ms / max(1, len(recs)),
+                    tflops=fl / (ms * 1e-3) / 1e12 if ms else 0.0, flops_per_launch=fl / max(1, len(recs)))
+    c = agg(convs)
+    c["algo_bytes_per_launch"] = sum(conv_bytes) / max(1, len(conv_bytes))
+    return c, agg(attns), agg(blocks)
 
 
-def cpu_baseline(unet, vae, seconds_budget=40.0):
+def traffic_per_call():
+    """Measured HBM bytes per ls_conv2d call (scripts/pmc_traffic.py over two
+    rocprofv3 --pmc passes of this bench, committed under profiles/)."""
+    p = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    return round(json.load(open(p))["hbm_bytes_per_call"])
+
+
+def cpu_baseline(unet, vae, R=256, steps=20, Bu=1):
     """The oracle (plain PyTorch fp32 restatement, oracle/ref_cpu.py) on host cores:
-    one full-size UNet forward at F=16 + VAE encode/decode of one frame, scaled
-    to the window (20 UNet + 32 encodes + 16 decodes)."""
-    from oracle import ref_cpu as R
+    one full-size UNet forward at F=16 (B=1) + VAE encode/decode of one frame,
+    scaled to the window (steps x Bu UNet + 32 encodes + 16 decodes)."""
+    from oracle import ref_cpu as O
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     usd, vsd = unet._sd, vae._sd
     g = torch.Generator().manual_seed(0)
-    sample = torch.randn((1, 13, 16, 32, 32), generator=g)
+    h = R // 8
+    sample = torch.randn((1, 13, 16, h, h), generator=g)
     audio = torch.randn((16, 50, 384), generator=g)
-    x = torch.rand((1, 3, 256, 256), generator=g) * 2 - 1
+    x = torch.rand((1, 3, R, R), generator=g) * 2 - 1
     with torch.no_grad():
         t0 = time.perf_counter()
-        R.unet_forward(usd, STAGE2_MODEL, sample, 951, audio)
+        O.unet_forward(usd, STAGE2_MODEL, sample, 951, audio)
         t_unet = time.perf_counter() - t0
         t0 = time.perf_counter()
-        R.vae_encode_moments(vsd, x)
+        O.vae_encode_moments(vsd, x)
         t_enc = time.perf_counter() - t0
         t0 = time.perf_counter()
-        R.vae_decode(vsd, torch.randn((1, 4, 32, 32), generator=g))
+        O.vae_decode(vsd, torch.randn((1, 4, h, h), generator=g))
         t_dec = time.perf_counter() - t0
-    t_window = 20 * t_unet + 32 * t_enc + 16 * t_dec
+    t_window = steps * Bu * t_unet + 32 * t_enc + 16 * t_dec
     return dict(value=16.0 / t_window, unit="frames/s", cores=threads, kind="port",
-                sample=f"1 UNet fwd (F=16) {t_unet:.2f}s + 1-frame VAE enc {t_enc:.2f}s + dec {t_dec:.2f}s, "
-                       f"scaled to 20 UNet + 32 enc + 16 dec per 16-frame window (oracle/ref_cpu.py fp32)")
+                sample=f"{R}x{R}: 1 UNet fwd (B=1, F=16) {t_unet:.2f}s + 1-frame VAE enc {t_enc:.2f}s + dec "
+                       f"{t_dec:.2f}s, scaled to {steps}x{Bu} UNet + 32 enc + 16 dec per 16-frame window "
+                       "(oracle/ref_cpu.py fp32)")
 
 
 def main():
@@ -124,14 +185,24 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--guidance", type=float, default=1.0)
-    ap.add_argument("--inference-steps", type=int, default=20)
+    ap.add_argument("--config", type=int, default=1, choices=sorted(PRESETS),
+                    help="BASELINE.json configs[i]: 1 = 256^2/20 steps/g 1.0 (headline), 2 = 50 steps/g 2.0 (CFG), "
+                         "4 = 512^2/20 steps")
+    ap.add_argument("--guidance", type=float, default=None)
+    ap.add_argument("--inference-steps", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graphs", action="store_true")
-    ap.add_argument("--windows-per-batch", type=int, default=8,
+    ap.add_argument("--windows-per-batch", type=int, default=None,
                     help="independent 16-frame windows batched through one UNet call per DDIM step")
     ap.add_argument("--no-single-window", action="store_true", help="skip the 1-window latency leg")
     args = ap.parse_args()
+    pre = PRESETS[args.config]
+    if args.guidance is None:
+        args.guidance = pre["guidance"]
+    if args.inference_steps is None:
+        args.inference_steps = pre["steps"]
+    if args.windows_per_batch is None:
+        args.windows_per_batch = pre["windows"]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -142,7 +213,7 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
 
-    F, R = 16, 256
+    F, R = 16, pre["resolution"]
     h = R // 8
     unet = UNet3DConditionModel(**STAGE2_MODEL).init_weights(41).to(device).eval()
     vae = AutoencoderKL().init_weights(51).to(device)
@@ -187,7 +258,7 @@ def main():
         elapsed = float(t.item())
     window_ms = sum(a.elapsed_time(b) for a, b in ev_step) / K
 
-    probe = conv_probe(unet, eng, device)
+    probe, attn_probe, blk_probe = step_probe(eng, device)
     single = None
     if rank == 0 and nw > 1 and not args.no_single_window:
         # latency of ONE window alone (same kernels, 16-frame batch) for reference
@@ -204,15 +275,16 @@ def main():
         del e1w
     frames = world * K * FB
     value = frames / elapsed
-    tf_per_frame = (args.inference_steps * UNET_TF * (2 if args.guidance > 1 else 1) + 32 * VAE_ENC_TF
-                    + 16 * VAE_DEC_TF) / 16
+    Bu = 2 if args.guidance > 1 else 1
+    unet_tf, enc_tf, dec_tf = WORK_TF[R]
+    tf_per_frame = (args.inference_steps * unet_tf * Bu + 32 * enc_tf + 16 * dec_tf) / 16
     if rank == 0:
         res = {
-            "metric": "lip-synced frames/sec at 256x256, 16-frame window, 20 DDIM steps",
+            "metric": f"lip-synced frames/sec at {R}x{R}, 16-frame window, {args.inference_steps} DDIM steps",
             "value": round(value, 3), "unit": "frames/s", "n_gpus": world, "steps": K, "warmup": W,
             "ms_per_step": round(elapsed / K * 1e3, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic (seeded faces/audio/noise, random-init weights)",
-            "config": {"workload": f"configs[{1 if args.guidance <= 1 else 2}]: 256x256 x16-frame windows, "
+            "config": {"workload": f"configs[{args.config}]: {R}x{R} x16-frame windows, "
                                    f"{args.inference_steps} DDIM steps, guidance {args.guidance}, "
                                    "LatentSync-1.5 UNet + SD-VAE, bf16; "
                                    f"{nw} independent windows of a clip batched per UNet call",
@@ -222,14 +294,25 @@ def main():
             "batch_ms_gpu_events": round(window_ms, 3),
             "single_window": single,
             "window_mfma_frac": round(tf_per_frame * value / world / PEAK_BF16_TF, 4),
-            "roofline": {"bound": "mfma", "kernel": "conv_gemm_kernel (all ls_conv2d launches of one UNet fwd)",
+            "roofline": {"bound": "mfma",
+                         "kernel": "conv_gemm family: every ls_conv2d call of one UNet fwd (conv_gemm_* GEMM + split-K reduce)",
                          "achieved": round(probe["tflops"], 2), "peak": PEAK_BF16_TF, "unit": "TFLOP/s",
-                         "frac": round(probe["tflops"] / PEAK_BF16_TF, 4), "traffic": None,
+                         "frac": round(probe["tflops"] / PEAK_BF16_TF, 4), "traffic": traffic_per_call(),
+                         "traffic_unit": "HBM bytes per ls_conv2d call (rocprofv3 PMC, profiles/pmc_traffic.json)",
                          "launches": probe["launches"], "avg_launch_ms": round(probe["avg_ms"], 4),
-                         "flops_per_launch": probe["flops_per_launch"]},
+                         "flops_per_launch": probe["flops_per_launch"],
+                         "algorithmic_bytes_per_launch": round(probe["algo_bytes_per_launch"])},
+            "attention": {"kernel": "ls_attention (SDPA: spatial self, audio cross, temporal)",
+                          "achieved_tflops": round(attn_probe["tflops"], 2), "launches": attn_probe["launches"],
+                          "avg_launch_ms": round(attn_probe["avg_ms"], 4),
+                          "frac": round(attn_probe["tflops"] / PEAK_BF16_TF, 4),
+                          "blocks": "Transformer3DModel + motion modules (a14-a17): GEMM + SDPA FLOPs / block wall time",
+                          "blocks_tflops": round(blk_probe["tflops"], 2), "blocks_n": blk_probe["launches"],
+                          "blocks_ms": round(blk_probe["total_ms"], 3),
+                          "blocks_mfma_frac": round(blk_probe["tflops"] / PEAK_BF16_TF, 4)},
         }
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(unet, vae)
+            res["cpu_baseline"] = cpu_baseline(unet, vae, R, args.inference_steps, Bu)
             res["speedup_vs_cpu"] = round(value / res["cpu_baseline"]["value"], 1)
         print(json.dumps(res), flush=True)
     if world > 1:

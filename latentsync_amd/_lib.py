@@ -89,7 +89,7 @@ def load(path: str = None):
     global _lib
     if _lib is not None:
         return _lib
-    path = path or LIB_PATH
+    path = path or os.environ.get("LS_HIP_LIB") or LIB_PATH  # LS_HIP_LIB: A/B builds in tools
     if not os.path.exists(path):
         raise RuntimeError(f"libls_hip.so not found at {path}: run `python -m latentsync_amd.build` "
                            "(the HIP library is required; there is no fallback path)")

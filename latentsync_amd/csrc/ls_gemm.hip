@@ -28,7 +28,7 @@ struct ConvArgs {
   void* y; int ldy; int y_f32;
   int ktiles, kt_per_split, split; float* partial;
   int ntm, ntn;
-  int ablate;  // tuning only: 1 = skip MFMAs, 2 = skip operand DMA
+  int ablate;  // tuning only (bits): 2 = skip operand DMA, 4 = skip epilogue stores
 };
 
 // ---------------------------------------------------------------- epilogue
@@ -177,6 +177,157 @@ __device__ __forceinline__ uint4 load_a_chunk(const ConvArgs& a, int kt, int ch,
 
 __device__ __forceinline__ int swz(int row, int ch) { return row * 8 + (ch ^ ((row >> 1) & 7)); }
 
+// Accumulators of wave-row p -> LDS staging (fp32, pitch BN + 4).
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void stage_acc(f32x4 (&acc)[BM / WM / 16][BN / WN / 16], float* st, int p) {
+  constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16, SP = BN + 4;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (wid / WN != p) return;
+  const int wn = wid % WN;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        st[(i * 16 + (lane >> 4) * 4 + r) * SP + wn * WTN + j * 16 + (lane & 15)] = acc[i][j][r];
+}
+
+// Vectorised single-pass epilogue (N % 8 == 0, no split-K).  Every thread owns
+// ONE 8-column chunk of the tile for the whole epilogue, so the per-column side
+// inputs (bias, LayerNorm colsum) are loaded once, before the first barrier; the
+// per-row side inputs (residual, row vector, LayerNorm row stats) of all of a
+// thread's rows in a wave-row pass are issued together before any is consumed --
+// one L2/HBM round trip per pass instead of one per chunk.
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void store_tile_plain(const ConvArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
+                                                 float* st, int m0, int n0) {
+  constexpr int NT = WM * WN * 64, WTM = BM / WM, SP = BN + 4;
+  constexpr int CPRW = BN / 8;                 // chunk columns per tile row
+  constexpr int RPI = NT / CPRW;               // rows per iteration
+  constexpr int ITER = (WTM + RPI - 1) / RPI;  // iterations per wave-row pass
+  const int tid = threadIdx.x;
+  const int c8 = (tid % CPRW) * 8, r0 = tid / CPRW;
+  const int col = n0 + c8;
+  const bool cok = (r0 < RPI) && col < a.N;
+  // row vector (per-frame temb / positional-encoding rows): one row for the whole
+  // tile in the common case (rows_per_vec >= the tile's row span), folded into
+  // the per-column constants; otherwise looked up per row.
+  const bool rv_tile = a.rowvec && m0 / a.rows_per_vec == (min(m0 + BM, a.M) - 1) / a.rows_per_vec;
+  float bb[8], cs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { bb[j] = 0.f; cs[j] = 0.f; }
+  if (cok && a.bias) load8f(a.bias + col, bb);
+  if (cok && rv_tile) {
+    float rv[8];
+    load8f(a.rowvec + rv_row(a, m0) + col, rv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bb[j] += rv[j];
+  }
+  if (cok && a.ln_mr) load8f(a.ln_cs + col, cs);
+#pragma unroll 1
+  for (int p = 0; p < WM; ++p) {
+    stage_acc<BM, BN, WM, WN>(acc, st, p);
+    const int rbase = m0 + p * WTM;
+    float2 mr[ITER];
+    uint4 rs[ITER];
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int rl = r0 + it * RPI, row = rbase + rl;
+      const bool ok = cok && rl < WTM && row < a.M;
+      mr[it] = make_float2(0.f, 1.f);
+      rs[it] = make_uint4(0, 0, 0, 0);
+      if (ok && a.ln_mr) mr[it] = *(const float2*)(a.ln_mr + 2L * row);
+      if (ok && a.res) rs[it] = *(const uint4*)(a.res + (long)row * a.ldr + col);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int rl = r0 + it * RPI, row = rbase + rl;
+      if (!(cok && rl < WTM && row < a.M)) continue;
+      const float* s = st + rl * SP + c8;
+      const float4 s0 = *(const float4*)s, s1 = *(const float4*)(s + 4);
+      float v[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      float r8[8], rv[8];
+      unpack8(rs[it], r8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) rv[j] = 0.f;
+      if (a.rowvec && !rv_tile) load8f(a.rowvec + rv_row(a, row) + col, rv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = mr[it].y * (v[j] - mr[it].x * cs[j]);
+        v[j] = act_fn(a.act, (x + bb[j] + rv[j] + r8[j]) * a.out_scale);
+      }
+      if (a.ablate & 4) {
+        if (v[0] == 12345.f) ((float*)a.y)[0] = v[1];
+      } else if (a.y_f32) {
+        float* y = (float*)a.y + (long)row * a.ldy + col;
+        *(float4*)y = make_float4(v[0], v[1], v[2], v[3]);
+        *(float4*)(y + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      } else {
+        *(uint4*)((u16*)a.y + (long)row * a.ldy + col) = pack8(v);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// GEGLU variant: a thread owns one 8-wide OUTPUT chunk, i.e. packed columns
+// [ph, ph+8) (h) and [ph+16, ph+24) (g) of the 16-row-interleaved W1.
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void store_tile_geglu(const ConvArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
+                                                 float* st, int m0, int n0) {
+  constexpr int NT = WM * WN * 64, WTM = BM / WM, SP = BN + 4;
+  constexpr int CPRW = BN / 16;
+  constexpr int RPI = NT / CPRW;
+  constexpr int ITER = (WTM + RPI - 1) / RPI;
+  const int tid = threadIdx.x;
+  const int o8 = (tid % CPRW) * 8, r0 = tid / CPRW;
+  const int ph = (o8 >> 4) * 32 + (o8 & 15);
+  const int col = n0 + ph;                       // packed column of h
+  const int oc = (col >> 5) * 16 + (col & 15);   // output column
+  const bool cok = (r0 < RPI) && col < a.N;
+  float bh[8], bg[8], ch[8], cg[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { bh[j] = 0.f; bg[j] = 0.f; ch[j] = 0.f; cg[j] = 0.f; }
+  if (cok && a.bias) { load8f(a.bias + col, bh); load8f(a.bias + col + 16, bg); }
+  if (cok && a.ln_mr) { load8f(a.ln_cs + col, ch); load8f(a.ln_cs + col + 16, cg); }
+#pragma unroll 1
+  for (int p = 0; p < WM; ++p) {
+    stage_acc<BM, BN, WM, WN>(acc, st, p);
+    const int rbase = m0 + p * WTM;
+    float2 mr[ITER];
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int rl = r0 + it * RPI, row = rbase + rl;
+      mr[it] = make_float2(0.f, 1.f);
+      if (cok && rl < WTM && row < a.M && a.ln_mr) mr[it] = *(const float2*)(a.ln_mr + 2L * row);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int rl = r0 + it * RPI, row = rbase + rl;
+      if (!(cok && rl < WTM && row < a.M)) continue;
+      const float* s = st + rl * SP + ph;
+      float h[8], g[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        h[j] = mr[it].y * (s[j] - mr[it].x * ch[j]) + bh[j];
+        g[j] = mr[it].y * (s[16 + j] - mr[it].x * cg[j]) + bg[j];
+        h[j] *= gelu_erf(g[j]);
+      }
+      if (a.y_f32) {
+        float* y = (float*)a.y + (long)row * a.ldy + oc;
+        *(float4*)y = make_float4(h[0], h[1], h[2], h[3]);
+        *(float4*)(y + 4) = make_float4(h[4], h[5], h[6], h[7]);
+      } else {
+        *(uint4*)((u16*)a.y + (long)row * a.ldy + oc) = pack8(h);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // Stage the accumulator tile through LDS one wave-row (WTM rows) at a time, then
 // each thread handles whole 8-column chunks (split-K slab / GEGLU / plain).
 template <int BM, int BN, int WM, int WN>
@@ -190,6 +341,11 @@ __device__ __forceinline__ void store_tile(const ConvArgs& a, f32x4 (&acc)[BM / 
   const int wm = wid / WN, wn = wid % WN;
   const bool vec = (a.N % 8 == 0) && (a.ldy % 8 == 0) && (!a.res || a.ldr % 8 == 0);
   const bool geglu = a.act == LS_ACT_GEGLU;
+  if (a.split == 1 && vec) {
+    if (geglu) store_tile_geglu<BM, BN, WM, WN>(a, acc, st, m0, n0);
+    else store_tile_plain<BM, BN, WM, WN>(a, acc, st, m0, n0);
+    return;
+  }
 #pragma unroll 1
   for (int p = 0; p < WM; ++p) {
     if (wm == p) {
@@ -480,7 +636,7 @@ __global__ void __launch_bounds__(256) conv_gemm_dma_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const bool do_dma = a.ablate != 2;
+  const bool do_dma = !(a.ablate & 2);
 #pragma unroll
   for (int t = 0; t < NST - 1; ++t)
     if (kt0 + t < kt1 && do_dma) issue(kt0 + t, t);

@@ -22,16 +22,25 @@ SHAPES = [  # (name, n_img, H, Cin, Cout, ksize, act)
 
 def run(tag, reps=20, scale=1):
     tot_f, tot_t = 0.0, 0.0
-    only = os.environ.get("GEMM_ONLY")
+    only = os.environ.get("GEMM_ONLY")  # comma-separated name substrings
     for name, n, H, cin, cout, ks, act in SHAPES:
-        if only and only not in name:
+        if only and not any(o in name for o in only.split(",")):
             continue
         n = n * scale
         x = torch.randn(n, H, H, cin, device="cuda").to(torch.bfloat16)
         w = torch.randn(cout, cin, ks, ks) / (cin * ks * ks) ** 0.5
         pw = ops.Packed(pack_weight(w).to(torch.bfloat16).cuda(), torch.zeros(cout, device="cuda"), cin, ks, cout,
                         geglu=act == 1)
-        out = ops.conv(x, pw, act=act)
+        kw = {}
+        epi = os.environ.get("GEMM_EPI", "")  # side inputs of the UNet's epilogues: res,rowvec,ln
+        if "res" in epi and act != 1:
+            kw["res"] = torch.randn(n, H, H, cout, device="cuda").to(torch.bfloat16)
+        if "rowvec" in epi:
+            kw["rowvec"] = (torch.randn(n // 16, pw.N, device="cuda"), 16 * H * H, pw.N)
+        if "ln" in epi and ks == 1 and cin <= 2048:
+            pw.colsum = pw.w.float().sum(1).contiguous()
+            kw["ln_stats"] = ops.row_stats(x.view(-1, cin))
+        out = ops.conv(x, pw, act=act, **kw)
         torch.cuda.synchronize()
         # graph of 10 launches: GPU time without host submission gaps
         g = torch.cuda.CUDAGraph()
@@ -40,7 +49,7 @@ def run(tag, reps=20, scale=1):
         with torch.cuda.stream(s):
             with torch.cuda.graph(g, stream=s):
                 for _ in range(10):
-                    ops.conv(x, pw, act=act, out=out)
+                    ops.conv(x, pw, act=act, out=out, **kw)
         torch.cuda.current_stream().wait_stream(s)
         g.replay()
         torch.cuda.synchronize()
@@ -60,8 +69,13 @@ if __name__ == "__main__":
     # modes: dma reg nomfma nodma bk32 t1..t6 (forced tile id); suffix @4 = 4x the frames
     for arg in sys.argv[1:] or ["dma"]:
         mode, _, sc = arg.partition("@")
-        lib.ls_set_tuning(1, 1 if mode == "reg" else 0)
-        lib.ls_set_tuning(4, {"nomfma": 1, "nodma": 2}.get(mode, 0))
-        lib.ls_set_tuning(5, 32 if mode == "bk32" else 64)
-        lib.ls_set_tuning(2, int(mode[1:]) if mode.startswith("t") else 0)
+        # mode parts joined by '+': reg, bk32, tN (forced tile id), abN (ablation bits), nomfma, nodma
+        parts = mode.split("+")
+        ab = {"nomfma": 1, "nodma": 2}.get(mode, 0)
+        ab |= sum(int(p[2:]) for p in parts if p.startswith("ab"))
+        tile = [int(p[1:]) for p in parts if p.startswith("t") and p[1:].isdigit()]
+        lib.ls_set_tuning(1, 1 if "reg" in parts else 0)
+        lib.ls_set_tuning(4, ab)
+        lib.ls_set_tuning(5, 32 if "bk32" in parts else 64)
+        lib.ls_set_tuning(2, tile[0] if tile else 0)
         run(arg, scale=int(sc or 1))

@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU-box round check: gpu tests -> bench (default) -> rocprofv3 kernel stats of a short bench.
+# GPU-box round check: gpu tests -> bench (default config) -> rocprofv3 kernel stats of a short bench.
 # Stops at the first failure; every GPU step has its own time limit.
 # usage: bash scripts/gpu_full.sh TAG [bench args...]
 set -o pipefail

@@ -29,6 +29,12 @@ def main():
     for r in seg:
         if 'conv_gemm' in r['Kernel_Name']:
             agg2[(r['Kernel_Name'].split('(')[0].replace('void ls::conv_gemm_kernel', ''), r['Grid_Size_X'])].append(dur(r))
+    fam = [dur(r) for r in seg if 'conv_gemm' in r['Kernel_Name'] or 'splitk_reduce' in r['Kernel_Name']]
+    ncall = sum('conv_gemm' in r['Kernel_Name'] for r in seg)
+    print(f"conv_gemm family: {ncall} ls_conv2d calls (+{len(fam) - ncall} split-K reduces), total {sum(fam)/1e6:.3f} ms, "
+          f"avg per ls_conv2d call {sum(fam)/max(1, ncall)/1e3:.1f} us  (bench.py roofline.avg_launch_ms)")
+    att = [dur(r) for r in seg if 'attn' in r['Kernel_Name']]
+    print(f"attention kernels: {len(att)} launches, total {sum(att)/1e6:.3f} ms, avg {sum(att)/max(1,len(att))/1e3:.1f} us")
     print('--- gemm shapes')
     for k2, v in sorted(agg2.items(), key=lambda x: -sum(x[1]))[:int(sys.argv[2]) if len(sys.argv) > 2 else 20]:
         print(f"{sum(v)/1e6:7.3f} ms n={len(v):3d} avg {sum(v)/len(v)/1e3:7.1f}us {k2}")
