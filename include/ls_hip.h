@@ -232,6 +232,11 @@ int ls_add_rows(const uint16_t* x, int64_t rows, int32_t C, int32_t ldx, const f
  * key 4 = ablation (1 skip MFMA, 2 skip operand DMA; timing only); key 5 = DMA K-tile depth 32 or 64. */
 int ls_set_tuning(int32_t key, int32_t value);
 
+/* Diagnostics: workgroups per CU the runtime can co-schedule for a GEMM kernel
+ * instance (hipOccupancyMaxActiveBlocksPerMultiprocessor with its dynamic LDS):
+ * which 1 = 128x160 DMA tile, 2 = 256x256 8-wave tile, 3 = 128x128 DMA tile. */
+int ls_gemm_occupancy(int32_t which);
+
 /* Whisper log-mel spectrogram (whisper/audio.py:92-125: torch.stft n_fft 400, hop
  * 160, periodic Hann, centre/reflect padding, last frame dropped, |X|^2, mel
  * filterbank, log10 clamp 1e-10, clip-global max-8 floor, (x + 4) / 4).

@@ -72,6 +72,7 @@ _SIGS = {
     "ls_scale_latents": (C.c_int, [c_vp, C.c_int64, C.c_float, C.c_float, c_vp, C.c_int32, c_vp]),
     "ls_paste_back": (C.c_int, [c_vp, C.c_int32, c_vp, C.c_int32, c_vp, C.c_int32, C.c_int32, c_vp, c_vp, c_vp]),
     "ls_set_tuning": (C.c_int, [C.c_int32, C.c_int32]),
+    "ls_gemm_occupancy": (C.c_int, [C.c_int32]),
     "ls_log_mel_workspace_bytes": (C.c_size_t, [C.c_int64, C.c_int32]),
     "ls_log_mel": (C.c_int, [c_vp, C.c_int64, c_vp, C.c_int32, C.c_int64, c_vp, c_vp, C.c_size_t, c_vp]),
     "ls_audio_chunks": (C.c_int, [c_vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_double,

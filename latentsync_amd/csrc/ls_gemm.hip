@@ -28,7 +28,8 @@ struct ConvArgs {
   void* y; int ldy; int y_f32;
   int ktiles, kt_per_split, split; float* partial;
   int ntm, ntn;
-  int ablate;  // tuning only (bits): 2 = skip operand DMA, 4 = skip epilogue stores
+  int ablate;  // tuning only (bits): 2 = skip operand DMA, 4 = skip epilogue stores, 8 = skip epilogue,
+               // 16 = skip MFMAs (DMA kernel)
 };
 
 // ---------------------------------------------------------------- epilogue
@@ -199,7 +200,7 @@ __device__ __forceinline__ void stage_acc(f32x4 (&acc)[BM / WM / 16][BN / WN / 1
 // per-row side inputs (residual, row vector, LayerNorm row stats) of all of a
 // thread's rows in a wave-row pass are issued together before any is consumed --
 // one L2/HBM round trip per pass instead of one per chunk.
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, bool GEN>
 __device__ __forceinline__ void store_tile_plain(const ConvArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
                                                  float* st, int m0, int n0) {
   constexpr int NT = WM * WN * 64, WTM = BM / WM, SP = BN + 4;
@@ -256,11 +257,12 @@ __device__ __forceinline__ void store_tile_plain(const ConvArgs& a, f32x4 (&acc)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float x = mr[it].y * (v[j] - mr[it].x * cs[j]);
-        v[j] = act_fn(a.act, (x + bb[j] + rv[j] + r8[j]) * a.out_scale);
+        v[j] = (x + bb[j] + rv[j] + r8[j]) * a.out_scale;
+        if (GEN) v[j] = act_fn(a.act, v[j]);
       }
       if (a.ablate & 4) {
         if (v[0] == 12345.f) ((float*)a.y)[0] = v[1];
-      } else if (a.y_f32) {
+      } else if (GEN && a.y_f32) {
         float* y = (float*)a.y + (long)row * a.ldy + col;
         *(float4*)y = make_float4(v[0], v[1], v[2], v[3]);
         *(float4*)(y + 4) = make_float4(v[4], v[5], v[6], v[7]);
@@ -274,7 +276,7 @@ __device__ __forceinline__ void store_tile_plain(const ConvArgs& a, f32x4 (&acc)
 
 // GEGLU variant: a thread owns one 8-wide OUTPUT chunk, i.e. packed columns
 // [ph, ph+8) (h) and [ph+16, ph+24) (g) of the 16-row-interleaved W1.
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, bool GEN>
 __device__ __forceinline__ void store_tile_geglu(const ConvArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
                                                  float* st, int m0, int n0) {
   constexpr int NT = WM * WN * 64, WTM = BM / WM, SP = BN + 4;
@@ -316,7 +318,7 @@ __device__ __forceinline__ void store_tile_geglu(const ConvArgs& a, f32x4 (&acc)
         g[j] = mr[it].y * (s[16 + j] - mr[it].x * cg[j]) + bg[j];
         h[j] *= gelu_erf(g[j]);
       }
-      if (a.y_f32) {
+      if (GEN && a.y_f32) {
         float* y = (float*)a.y + (long)row * a.ldy + oc;
         *(float4*)y = make_float4(h[0], h[1], h[2], h[3]);
         *(float4*)(y + 4) = make_float4(h[4], h[5], h[6], h[7]);
@@ -330,9 +332,26 @@ __device__ __forceinline__ void store_tile_geglu(const ConvArgs& a, f32x4 (&acc)
 
 // Stage the accumulator tile through LDS one wave-row (WTM rows) at a time, then
 // each thread handles whole 8-column chunks (split-K slab / GEGLU / plain).
-template <int BM, int BN, int WM, int WN>
+// EPI selects the epilogue compiled into a kernel instance (host: epi_kind()), so
+// the common instances carry only the code they run -- the fully general
+// epilogue is ~40 KB of code, and fetching it per tile cost more than the
+// MFMAs of a K = 320 tile.
+//   EPI_PLAIN: vectorised, no split-K, no activation, bf16 out (bias / rowvec /
+//              residual / LayerNorm fold as runtime options);
+//   EPI_GEGLU: the same for the GEGLU epilogue;
+//   EPI_ANY:   everything (split-K slabs, GELU/SiLU, fp32 out, ragged N).
+enum { EPI_PLAIN = 0, EPI_GEGLU = 1, EPI_ANY = 2 };
+
+template <int BM, int BN, int WM, int WN, int EPI = EPI_ANY>
 __device__ __forceinline__ void store_tile(const ConvArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16], float* st,
                                            int m0, int n0, int z) {
+  if constexpr (EPI == EPI_PLAIN) {
+    store_tile_plain<BM, BN, WM, WN, false>(a, acc, st, m0, n0);
+    return;
+  } else if constexpr (EPI == EPI_GEGLU) {
+    store_tile_geglu<BM, BN, WM, WN, false>(a, acc, st, m0, n0);
+    return;
+  }
   constexpr int NT = WM * WN * 64;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int FM = WTM / 16, FN = WTN / 16;
@@ -342,8 +361,8 @@ __device__ __forceinline__ void store_tile(const ConvArgs& a, f32x4 (&acc)[BM / 
   const bool vec = (a.N % 8 == 0) && (a.ldy % 8 == 0) && (!a.res || a.ldr % 8 == 0);
   const bool geglu = a.act == LS_ACT_GEGLU;
   if (a.split == 1 && vec) {
-    if (geglu) store_tile_geglu<BM, BN, WM, WN>(a, acc, st, m0, n0);
-    else store_tile_plain<BM, BN, WM, WN>(a, acc, st, m0, n0);
+    if (geglu) store_tile_geglu<BM, BN, WM, WN, true>(a, acc, st, m0, n0);
+    else store_tile_plain<BM, BN, WM, WN, true>(a, acc, st, m0, n0);
     return;
   }
 #pragma unroll 1
@@ -564,7 +583,7 @@ __device__ __forceinline__ int swz_bk(int row, int c) {
   return row * 4 + (c ^ ((-(row >> 2)) & 3));
 }
 
-template <int BM, int BN, int WM, int WN, int KS, bool TAPU, int NST, int BK>
+template <int BM, int BN, int WM, int WN, int KS, bool TAPU, int NST, int BK, int EPI>
 __global__ void __launch_bounds__(256) conv_gemm_dma_kernel(ConvArgs a) {
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int FM = WTM / 16, FN = WTN / 16;
@@ -662,19 +681,40 @@ __global__ void __launch_bounds__(256) conv_gemm_dma_kernel(ConvArgs a) {
       for (int j = 0; j < FN; ++j)
         bfr[ks][j] = __builtin_bit_cast(bf16x8, cur[BM * CPR + swz_bk<BK>(wn * WTN + j * 16 + (lane & 15), c)]);
     }
+#ifdef LS_GEMM_ABLATE
+    if (!(a.ablate & 16))
+#endif
+    {
 #pragma unroll
-    for (int ks = 0; ks < KSTEPS; ++ks)
+      for (int ks = 0; ks < KSTEPS; ++ks)
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bfr[ks][j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bfr[ks][j], acc[i][j], 0, 0, 0);
+    }
+#ifdef LS_GEMM_ABLATE
+    else if (a.ablate & 32) {
+      acc[0][0][0] += (float)af[0][0][0] + (float)bfr[0][0][0];
+    }
+#endif
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     stage = stage + 1 == NST ? 0 : stage + 1;
   }
-  store_tile<BM, BN, WM, WN>(a, acc, (float*)lds, m0, n0, z);
+#ifdef LS_GEMM_ABLATE  // diagnostic build only (hipcc -DLS_GEMM_ABLATE): it costs registers
+  if (a.ablate & 8) {  // tuning: no epilogue at all (keep the accumulators live)
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) t += acc[i][j][0] + acc[i][j][3];
+    if (t == 12345.f) ((float*)a.y)[tid] = t;
+    return;
+  }
+#endif
+  store_tile<BM, BN, WM, WN, EPI>(a, acc, (float*)lds, m0, n0, z);
 }
 
 // 256-row tile, 8 waves (2 M x 4 N), each wave 128 x BN/4 (FM = 8 fragments of
@@ -684,7 +724,7 @@ __global__ void __launch_bounds__(256) conv_gemm_dma_kernel(ConvArgs a) {
 // barrier per K-tile; the next tile's DMA is issued right after the barrier so
 // it has a whole K-tile of MFMAs to land.  MFMA runs are bracketed by
 // s_setprio(1) so the co-resident wave's fragment reads interleave.
-template <int BN, int KS, bool TAPU>
+template <int BN, int KS, bool TAPU, int EPI>
 __global__ void __launch_bounds__(512) conv_gemm_big_kernel(ConvArgs a) {
   constexpr int BM = 256, BK = 64, WM = 2, WN = 4;
   constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -805,7 +845,7 @@ __global__ void __launch_bounds__(512) conv_gemm_big_kernel(ConvArgs a) {
   }
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  store_tile<BM, BN, WM, WN>(a, acc, (float*)lds, m0, n0, z);
+  store_tile<BM, BN, WM, WN, EPI>(a, acc, (float*)lds, m0, n0, z);
 }
 
 // 256 x 256 x 64 tile, 8 waves (2 M x 4 N, 128 x 64 per wave), phased schedule
@@ -1164,37 +1204,59 @@ static TileCfg pick_tile(long M, int N, int ktiles, bool allow_split, bool big_o
   return best;
 }
 
-template <int BM, int BN, int WM, int WN, int KS, bool TAPU, int NST, int BK>
+// epilogue variant of a launch (see store_tile)
+static int epi_kind(const ConvArgs& a) {
+  const bool vec = (a.N % 8 == 0) && (a.ldy % 8 == 0) && (!a.res || a.ldr % 8 == 0);
+  if (a.split != 1 || !vec || a.y_f32) return EPI_ANY;
+  if (a.act == LS_ACT_NONE) return EPI_PLAIN;
+  if (a.act == LS_ACT_GEGLU) return EPI_GEGLU;
+  return EPI_ANY;
+}
+
+template <int BM, int BN, int WM, int WN, int KS, bool TAPU, int NST, int BK, int EPI>
 static void launch_dma1(const ConvArgs& a, int grid, hipStream_t s) {
   // staging for the epilogue must fit too
   const size_t shm = std::max<size_t>((size_t)NST * (BM + BN) * (BK / 8) * 16, (size_t)(BM / WM) * (BN + 4) * 4);
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)conv_gemm_dma_kernel<BM, BN, WM, WN, KS, TAPU, NST, BK>,
+    (void)hipFuncSetAttribute((const void*)conv_gemm_dma_kernel<BM, BN, WM, WN, KS, TAPU, NST, BK, EPI>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     attr = true;
   }
-  conv_gemm_dma_kernel<BM, BN, WM, WN, KS, TAPU, NST, BK><<<grid, 256, shm, s>>>(a);
+  conv_gemm_dma_kernel<BM, BN, WM, WN, KS, TAPU, NST, BK, EPI><<<grid, 256, shm, s>>>(a);
 }
 
 template <int BM, int BN, int WM, int WN, int KS, bool TAPU>
 static void launch_dma(const ConvArgs& a, int grid, hipStream_t s) {
   if constexpr (BN >= 64) {
-    if (g_bk == 32) { launch_dma1<BM, BN, WM, WN, KS, TAPU, 3, 32>(a, grid, s); return; }
+    if (g_bk == 32) { launch_dma1<BM, BN, WM, WN, KS, TAPU, 3, 32, EPI_ANY>(a, grid, s); return; }
   }
-  launch_dma1<BM, BN, WM, WN, KS, TAPU, 2, 64>(a, grid, s);
+  switch (epi_kind(a)) {
+    case EPI_PLAIN: launch_dma1<BM, BN, WM, WN, KS, TAPU, 2, 64, EPI_PLAIN>(a, grid, s); break;
+    case EPI_GEGLU: launch_dma1<BM, BN, WM, WN, KS, TAPU, 2, 64, EPI_GEGLU>(a, grid, s); break;
+    default: launch_dma1<BM, BN, WM, WN, KS, TAPU, 2, 64, EPI_ANY>(a, grid, s);
+  }
+}
+
+template <int BN, int KS, bool TAPU, int EPI>
+static void launch_big2(const ConvArgs& a, int grid, hipStream_t s) {
+  const size_t shm = std::max<size_t>((size_t)2 * (256 + BN) * 8 * 16, (size_t)128 * (BN + 4) * 4);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv_gemm_big_kernel<BN, KS, TAPU, EPI>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    attr = true;
+  }
+  conv_gemm_big_kernel<BN, KS, TAPU, EPI><<<grid, 512, shm, s>>>(a);
 }
 
 template <int BN, int KS, bool TAPU>
 static void launch_big1(const ConvArgs& a, int grid, hipStream_t s) {
-  const size_t shm = std::max<size_t>((size_t)2 * (256 + BN) * 8 * 16, (size_t)128 * (BN + 4) * 4);
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)conv_gemm_big_kernel<BN, KS, TAPU>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)shm);
-    attr = true;
+  switch (epi_kind(a)) {
+    case EPI_PLAIN: launch_big2<BN, KS, TAPU, EPI_PLAIN>(a, grid, s); break;
+    case EPI_GEGLU: launch_big2<BN, KS, TAPU, EPI_GEGLU>(a, grid, s); break;
+    default: launch_big2<BN, KS, TAPU, EPI_ANY>(a, grid, s);
   }
-  conv_gemm_big_kernel<BN, KS, TAPU><<<grid, 512, shm, s>>>(a);
 }
 
 template <int KS, bool TAPU>
@@ -1202,7 +1264,7 @@ static void launch_big4(const ConvArgs& a, int grid, hipStream_t s) {
   const size_t shm = std::max<size_t>((size_t)4 * (256 + 256) * 4 * 16, (size_t)128 * (256 + 4) * 4);
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)conv_gemm_big4_kernel<KS, TAPU>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)conv_gemm_big4_kernel<KS, TAPU>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)shm);
     attr = true;
   }
@@ -1214,7 +1276,7 @@ static void launch_p8_1(const ConvArgs& a, int grid, hipStream_t s) {
   const size_t shm = std::max<size_t>((size_t)2 * 4 * 128 * 8 * 16, (size_t)128 * (256 + 4) * 4);
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)conv_gemm_p8_kernel<KS, TAPU>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)conv_gemm_p8_kernel<KS, TAPU>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)shm);
     attr = true;
   }
@@ -1302,6 +1364,25 @@ extern "C" int ls_set_tuning(int32_t key, int32_t value) {
     case 4: g_ablate = value; return LS_OK;
     case 5: if (value != 32 && value != 64) return fail(LS_ERR_INVALID, "BK 32 or 64"); g_bk = value; return LS_OK;
     default: return fail(LS_ERR_INVALID, "ls_set_tuning: unknown key");
+  }
+}
+
+template <typename K>
+static int occ(K kern, int threads, size_t shm) {
+  int n = 0;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, threads, shm) != hipSuccess) return -1;
+  return n;
+}
+
+extern "C" int ls_gemm_occupancy(int32_t which) {
+  switch (which) {
+    case 1: return occ(conv_gemm_dma_kernel<128, 160, 2, 2, 1, false, 2, 64, EPI_PLAIN>, 256,
+                       (size_t)2 * (128 + 160) * 8 * 16);
+    case 2: return occ(conv_gemm_big_kernel<256, 1, false, EPI_PLAIN>, 512, (size_t)2 * (256 + 256) * 8 * 16);
+    case 3: return occ(conv_gemm_dma_kernel<128, 128, 2, 2, 1, false, 2, 64, EPI_PLAIN>, 256,
+                       (size_t)2 * (128 + 128) * 8 * 16);
+    default: return fail(LS_ERR_INVALID, "ls_gemm_occupancy: which 1..3");
   }
 }
 

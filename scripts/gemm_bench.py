@@ -20,6 +20,9 @@ SHAPES = [  # (name, n_img, H, Cin, Cout, ksize, act)
 ]
 
 
+TORCH_REF = False
+
+
 def run(tag, reps=20, scale=1):
     tot_f, tot_t = 0.0, 0.0
     only = os.environ.get("GEMM_ONLY")  # comma-separated name substrings
@@ -40,7 +43,15 @@ def run(tag, reps=20, scale=1):
         if "ln" in epi and ks == 1 and cin <= 2048:
             pw.colsum = pw.w.float().sum(1).contiguous()
             kw["ln_stats"] = ops.row_stats(x.view(-1, cin))
-        out = ops.conv(x, pw, act=act, **kw)
+        if TORCH_REF:  # vendor library (hipBLASLt via torch.matmul) on the same GEMM: M x K @ K x N
+            xa = torch.randn(n * H * H, cin * ks * ks, device="cuda").to(torch.bfloat16)
+            wb = torch.randn(cin * ks * ks, cout, device="cuda").to(torch.bfloat16)
+            out = torch.empty(n * H * H, cout, device="cuda", dtype=torch.bfloat16)
+            launch = lambda: torch.matmul(xa, wb, out=out)
+        else:
+            out = ops.conv(x, pw, act=act, **kw)
+            launch = lambda: ops.conv(x, pw, act=act, out=out, **kw)
+        launch()
         torch.cuda.synchronize()
         # graph of 10 launches: GPU time without host submission gaps
         g = torch.cuda.CUDAGraph()
@@ -49,7 +60,7 @@ def run(tag, reps=20, scale=1):
         with torch.cuda.stream(s):
             with torch.cuda.graph(g, stream=s):
                 for _ in range(10):
-                    ops.conv(x, pw, act=act, out=out, **kw)
+                    launch()
         torch.cuda.current_stream().wait_stream(s)
         g.replay()
         torch.cuda.synchronize()
@@ -78,4 +89,5 @@ if __name__ == "__main__":
         lib.ls_set_tuning(4, ab)
         lib.ls_set_tuning(5, 32 if "bk32" in parts else 64)
         lib.ls_set_tuning(2, tile[0] if tile else 0)
+        TORCH_REF = "torch" in parts
         run(arg, scale=int(sc or 1))

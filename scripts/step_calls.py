@@ -1,0 +1,95 @@
+"""Per-call HIP-event table of one UNet denoising step (eager launches, same
+kernels as the captured graph): every ls_conv2d / ls_attention / GroupNorm /
+LayerNorm call with its shape, time and TF/s, aggregated by shape.
+
+    python scripts/step_calls.py [windows] [resolution]
+"""
+import collections
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from latentsync_amd import ops  # noqa: E402
+from latentsync_amd.config import STAGE2_MODEL  # noqa: E402
+from latentsync_amd.pipeline import WindowEngine, load_fixed_mask  # noqa: E402
+from latentsync_amd.scheduler import DDIMScheduler  # noqa: E402
+from latentsync_amd.unet import UNet3DConditionModel  # noqa: E402
+from latentsync_amd.vae import AutoencoderKL  # noqa: E402
+
+
+def main():
+    nw = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    R = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+    dev = torch.device("cuda", 0)
+    unet = UNet3DConditionModel(**STAGE2_MODEL).init_weights(41).to(dev).eval()
+    vae = AutoencoderKL().init_weights(51).to(dev)
+    eng = WindowEngine(unet, vae, DDIMScheduler(**bench.SCHED_CFG), 16, R, 20, 1.0, use_graphs=False, windows=nw)
+    faces, audio, init, em, er = bench.synthetic_window(16 * nw, R, R // 8, 384, 1000, dev)
+    eng.load(faces, load_fixed_mask(R).to(dev), audio, init, em, er)
+    eng._step()
+    torch.cuda.synchronize()
+    recs = []
+
+    def ev():
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(torch.cuda.current_stream())
+        return e
+
+    names = ["conv", "attention", "group_norm", "group_norm_apply", "row_stats"]
+    orig = {n: getattr(ops, n) for n in names}
+
+    def wrap(n):
+        def f(*a, **kw):
+            e0 = ev()
+            r = orig[n](*a, **kw)
+            e1 = ev()
+            if n == "conv":
+                x, pw = a[0], a[1]
+                x2 = kw.get("x2")
+                cin = x.shape[-1] + (x2.shape[-1] if x2 is not None else 0)
+                y = r
+                M = y.shape[0] * y.shape[1] * y.shape[2]
+                fl = 2.0 * M * pw.N * cin * pw.ksize ** 2
+                key = (n, f"M={M} N={pw.N} K={cin * pw.ksize ** 2} ks={pw.ksize} act={kw.get('act', 0)} "
+                          f"res={int(kw.get('res') is not None)} ln={int(kw.get('ln_stats') is not None)} "
+                          f"up={int(kw.get('upsample', False))} s={kw.get('stride', 1)}")
+            elif n == "attention":
+                fl = 4.0 * kw["batch"] * kw["heads"] * kw["nq"] * kw["nk"] * kw["head_dim"]
+                key = (n, f"b={kw['batch']} h={kw['heads']} nq={kw['nq']} nk={kw['nk']} d={kw['head_dim']}")
+            else:
+                fl = 0.0
+                key = (n, f"shape={tuple(a[0].shape)}")
+            recs.append((key, e0, e1, fl))
+            return r
+        return f
+
+    for n in names:
+        setattr(ops, n, wrap(n))
+    eng._step()
+    torch.cuda.synchronize()
+    for n in names:
+        setattr(ops, n, orig[n])
+    agg = collections.defaultdict(lambda: [0, 0.0, 0.0])
+    tot = 0.0
+    for key, e0, e1, fl in recs:
+        t = e0.elapsed_time(e1)
+        agg[key][0] += 1
+        agg[key][1] += t
+        agg[key][2] += fl
+        tot += t
+    print(f"step: {len(recs)} calls, {tot:.3f} ms summed (windows={nw}, R={R})")
+    fam = collections.defaultdict(float)
+    for (n, _), (c, t, fl) in agg.items():
+        fam[n] += t
+    for n, t in sorted(fam.items(), key=lambda x: -x[1]):
+        print(f"  {n:18s} {t:8.3f} ms")
+    for (n, k), (c, t, fl) in sorted(agg.items(), key=lambda x: -x[1][1]):
+        tf = fl / (t * 1e-3) / 1e12 if fl else 0.0
+        print(f"{t:8.3f} ms n={c:3d} avg {t / c * 1e3:8.1f} us {tf:7.1f} TF/s  {n:16s} {k}")
+
+
+if __name__ == "__main__":
+    main()
