@@ -6,6 +6,7 @@ build/ objects and links latentsync_amd/libls_hip.so.  No CUDA, no dual path.
 """
 import concurrent.futures as cf
 import os
+import re
 import subprocess
 import sys
 
@@ -15,7 +16,14 @@ CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(REPO, "build", "obj")
 LIB = os.path.join(HERE, "libls_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result", "-munsafe-fp-atomics"]
+# -fno-slp-vectorize: no v_pk_*_f32 packed fp32 math.  (1) Beside MFMAs it costs
+# issue cycles (MI355X_MICROARCH.md, 'price of one filler').  (2) Correctness: the
+# SLP-packed LayerNorm normalisation of the row-block GEMM (v_pk_fma_f32 with
+# op_sel picking one half of a VGPR pair whose other half was being recycled)
+# produced intermittently wrong values on gfx950 -- second wave of a SIMD, run to
+# run different -- and bit-exact results without packing (scripts/debug_rb3.py).
+FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result", "-munsafe-fp-atomics",
+         "-fno-slp-vectorize"]
 
 
 def _deps():
@@ -24,13 +32,36 @@ def _deps():
     return max(os.path.getmtime(h) for h in hdrs)
 
 
+# Kernels that pace their operand DMA with counted `s_waitcnt vmcnt(N)`: a register
+# (VGPR) spill adds scratch loads/stores to the vmcnt queue and silently breaks the count,
+# so the build refuses any spill in them (hipcc resource-usage remarks).
+COUNTED_VMCNT = ("gemm_rowblock_kernel", "conv_gemm_dma_kernel")
+
+
+def _spills(stderr):
+    bad, cur = [], None
+    for line in stderr.splitlines():
+        m = re.search(r"remark: +Function Name: (\S+)", line)
+        if m:
+            cur = m.group(1)
+            continue
+        m = re.search(r"remark: +VGPRs Spill: (\d+)", line)
+        if m and cur and int(m.group(1)) > 0 and any(k in cur for k in COUNTED_VMCNT):
+            bad.append(f"{cur}: {line.split('remark:')[1].strip()}")
+    return bad
+
+
 def _compile(src, obj, dep_time):
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), dep_time):
         return obj, None
-    cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+    cmd = [HIPCC] + FLAGS + ["-Rpass-analysis=kernel-resource-usage", "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         return obj, r.stderr
+    bad = _spills(r.stderr)
+    if bad:
+        os.remove(obj)
+        return obj, "register spills in counted-vmcnt kernels:\n" + "\n".join(bad)
     return obj, None
 
 

@@ -12,6 +12,8 @@
 // current one).  LDS rows are 128 B (64 bf16) and XOR-swizzled at 16-B chunk
 // granularity (chunk ^ ((row >> 1) & 7)) so the ds_read_b128 fragment reads of
 // a 16-lane group hit 16 distinct 4-bank slots.
+#include <type_traits>
+
 #include "ls_common.h"
 
 namespace ls {
@@ -1169,6 +1171,224 @@ __global__ void splitk_reduce_kernel(ConvArgs a) {
   }
 }
 
+// ------------------------------------------------------------ row-block GEMM
+// The short-K linears of the 32x32 level (K = Cin = 320: Transformer/motion
+// proj_in/out, fused q|k|v, q, out-proj, GEGLU W1) are epilogue/bandwidth bound
+// on the tiled kernels: every 128x160 tile pays a full prologue + LDS-staged
+// epilogue for only 5 K-tiles of MFMAs, and re-reads its A rows once per N tile.
+// Here one workgroup (8 waves, 2 per SIMD) owns 256 rows x a range of N:
+//   * each wave keeps its 32 A rows x K in registers for the whole kernel
+//     (2 x KT bf16x8 fragments = 80 VGPRs at K = 320): A is read once;
+//   * W streams through LDS in 64-column chunks (all of K per chunk, 2-stage
+//     ring, global_load_lds DMA into the XOR-swizzled 64-wide images);
+//   * the product is computed transposed, C^T = W A^T (MFMA A operand = W rows,
+//     B operand = A rows), so a lane's accumulator holds 4 consecutive output
+//     columns of one row and the epilogue stores 8 B per lane straight from
+//     registers -- no LDS staging, no barrier -- and runs in the same basic
+//     block as the next chunk's MFMAs (double-buffered accumulators), so its
+//     VALU work and stores overlap the matrix pipe.
+// FLAGS: RB_LN LayerNorm fold (ln_rowstats/ln_colsum), RB_RES residual,
+// RB_RV row vector (positional-encoding rows), RB_GEGLU GEGLU epilogue.  With RB_LN the
+// register-resident A rows are normalised in place (the host folds gamma / beta).
+// Host contract (rowblock_ok): ksize 1, no x2 / affine prologue, K = 32*KT = Cin,
+// M % 256 == 0, N % 64 == 0, no split-K, bf16 output with 4-aligned pitches.
+enum { RB_LN = 1, RB_RES = 2, RB_RV = 4, RB_GEGLU = 8 };
+
+template <int KT, int FN, int FLAGS>
+__global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
+  constexpr int FM = 2, BN = 16 * FN;
+  constexpr int KTILES = KT / 2;              // 64-wide LDS images per chunk
+  constexpr int WIMG = BN * KTILES * 8;       // uint4 of the W images of a chunk
+  constexpr int STAGE = WIMG + 48;            // + bias / colsum / row-vector columns (3 x 64 fp32)
+  constexpr bool LN = FLAGS & RB_LN, RES = FLAGS & RB_RES, RV = FLAGS & RB_RV, GG = FLAGS & RB_GEGLU;
+  constexpr int NSTORE = GG ? FM * FN / 2 : FM * FN;
+  constexpr int PPT = (WIMG + 511) / 512;     // 16-B DMA pieces per thread per chunk
+  static_assert(KT % 2 == 0 && WIMG % 256 == 0, "K must be a multiple of 64");
+  extern __shared__ __attribute__((aligned(16))) uint4 lds_dyn[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l16 = lane & 15, lg = lane >> 4;
+  const int rb = blockIdx.x / a.ntn, ns = blockIdx.x - rb * a.ntn;
+  const int nch = a.N / BN;
+  const int c0 = (int)((long)nch * ns / a.ntn), c1 = (int)((long)nch * (ns + 1) / a.ntn);
+  const int mw = rb * 256 + wid * 32;  // this wave's first row
+
+  // chunk c -> LDS stage: W rows [64c, 64c + 64) x all K as KTILES swizzled 64-wide
+  // images, then the chunk's 64 bias, colsum and row-vector values (wave 0).
+  // piece q = p * 512 + tid of a chunk's images: image t = q / (8 BN), row (q / 8) % BN, chunk q % 8
+  const long rv_base = RV ? rv_row(a, rb * 256) : 0;  // host: rows_per_vec % 256 == 0
+  auto issue = [&](int c, int stage) {
+    uint4* dst = lds_dyn + stage * STAGE;
+#pragma unroll
+    for (int p = 0; p < PPT; ++p) {
+      const int q = p * 512 + tid, t = q / (8 * BN), row = (q >> 3) % BN, pc = q & 7;
+      const int lc = pc ^ ((row >> 1) & 7);  // logical 16-B chunk stored at physical chunk pc
+      if (WIMG % 512 == 0 || q < WIMG)       // (wave-uniform)
+        glds16(a.w + (long)(c * BN + row) * a.K + t * 64 + lc * 8, dst + p * 512 + wid * 64);
+    }
+    if (wid == 0 && lane < 48 && (lane & 15) * 4 < BN) {
+      const int q = lane >> 4, e = (lane & 15) * 4;
+      const float* base = q == 0 ? a.bias : q == 1 ? nullptr : (RV ? a.rowvec + rv_base : nullptr);
+      const void* ps = base ? (const void*)(base + c * BN + e) : (const void*)ls_zero_page;
+      glds16(ps, dst + WIMG);
+    }
+  };
+
+  if (c0 >= c1) return;
+  float2 mrow[FM];  // LayerNorm (mean, rstd) of this lane's two rows
+  if (LN) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) mrow[i] = *(const float2*)(a.ln_mr + 2L * (mw + i * 16 + l16));
+  }
+  issue(c0, 0);
+  // A rows -> registers (B operand of C^T = W A^T: lane = row l16, k = 8 lg .. + 7 of each 32-wide step)
+  bf16x8 ar[FM][KT];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const u16* src = a.x1 + (long)(mw + i * 16 + l16) * a.ld1 + lg * 8;
+#pragma unroll
+    for (int s = 0; s < KT; ++s) ar[i][s] = *(const bf16x8*)(src + s * 32);
+  }
+  if (LN) {
+    // LayerNorm applied to the register-resident A rows once ((x - mean) * rstd, rounded
+    // to bf16 like the reference's normalised activations); gamma / beta are folded
+    // into W and the bias on the host, so the epilogue needs no per-column colsum.
+    wait_vm<0>();
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const float rstd = mrow[i].y, nmr = -mrow[i].x * mrow[i].y;
+#pragma unroll
+      for (int s = 0; s < KT; ++s) {
+        bf16x8 v = ar[i][s];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (__bf16)fmaf((float)v[e], rstd, nmr);
+        ar[i][s] = v;
+      }
+    }
+  }
+  wait_vm<0>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  f32x4 acc0[FM][FN], acc1[FM][FN];
+  uint2 rs[FM][FN];
+
+  auto load_res = [&](int c) {
+    if (!RES) return;
+    const int nb = c * BN + 4 * lg;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        rs[i][j] = *(const uint2*)(a.res + (long)(mw + i * 16 + l16) * a.ldr + nb + 16 * j);
+  };
+  // column parameters (bias + row vector) of chunk c from its LDS stage, read before
+  // the next DMA is issued (an LDS read after it would wait for the DMA)
+  auto load_prm = [&](int stage, float4 (&bb)[FN]) {
+    const float4* prm = (const float4*)(lds_dyn + stage * STAGE + WIMG);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      bb[j] = prm[lg + 4 * j];
+      if (RV) {
+        const float4 r4 = prm[32 + lg + 4 * j];  // (FN 2 uses the first 8 of each 16)
+        bb[j].x += r4.x; bb[j].y += r4.y; bb[j].z += r4.z; bb[j].w += r4.w;
+      }
+    }
+  };
+  auto epilogue = [&](int c, const float4 (&bb)[FN], f32x4 (&acc)[FM][FN]) {
+    const int nb = c * BN + 4 * lg;  // packed column of fragment j: nb + 16 j
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        acc[i][j][0] += bb[j].x; acc[i][j][1] += bb[j].y; acc[i][j][2] += bb[j].z; acc[i][j][3] += bb[j].w;
+      }
+      u16* yrow = (u16*)a.y + (long)(mw + i * 16 + l16) * a.ldy;
+      if (GG) {
+#pragma unroll
+        for (int p = 0; p < FN / 2; ++p) {
+          float h[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) h[r] = acc[i][2 * p][r] * gelu_erf(acc[i][2 * p + 1][r]);
+          *(uint2*)(yrow + c * (BN / 2) + 16 * p + 4 * lg) = make_uint2(pack2(h[0], h[1]), pack2(h[2], h[3]));
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          float o[4];
+          float r4[4] = {0.f, 0.f, 0.f, 0.f};
+          if (RES) {
+            r4[0] = __uint_as_float(rs[i][j].x << 16); r4[1] = __uint_as_float(rs[i][j].x & 0xffff0000u);
+            r4[2] = __uint_as_float(rs[i][j].y << 16); r4[3] = __uint_as_float(rs[i][j].y & 0xffff0000u);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (acc[i][j][r] + r4[r]) * a.out_scale;
+          *(uint2*)(yrow + nb + 16 * j) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+        }
+      }
+    }
+  };
+  auto mfma_chunk = [&](int stage, f32x4 (&acc)[FM][FN]) {
+    const uint4* cur = lds_dyn + stage * STAGE;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KT; ++s) {
+      bf16x8 bw[FN];
+      const int ch = (s & 1) * 4 + lg;
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bw[j] = __builtin_bit_cast(bf16x8, cur[(s >> 1) * (8 * BN) + swz_bk<64>(j * 16 + l16, ch)]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], ar[i][s], acc[i][j], 0, 0, 0);
+    }
+  };
+  auto sync = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  // 3-stage ring: chunk c computes from stage c%3 while chunk c-1's parameters stay in
+  // (c-1)%3 for its epilogue and chunk c+1 lands in (c+1)%3.  Past the last chunk the DMA
+  // re-loads the last chunk into the spare stage, so the steady-state body is branch-free.
+  auto body = [&](int c, f32x4 (&acc)[FM][FN], f32x4 (&prev)[FM][FN]) {
+    const int st = (c - c0) % 3;
+    float4 bb[FN];
+    load_prm(st == 0 ? 2 : st - 1, bb);
+    load_res(c - 1);                                         // older than the DMA: waited on alone
+    issue(min(c + 1, c1 - 1), st == 2 ? 0 : st + 1);
+    mfma_chunk(st, acc);
+    epilogue(c - 1, bb, prev);
+    wait_vm<NSTORE>();                                       // the DMA (older than the stores) landed
+    sync();
+  };
+  // first chunk: no epilogue
+  issue(min(c0 + 1, c1 - 1), 1);
+  mfma_chunk(0, acc0);
+  wait_vm<0>();
+  sync();
+  int c = c0 + 1;
+  for (; c + 1 < c1; c += 2) {
+    body(c, acc1, acc0);
+    body(c + 1, acc0, acc1);
+  }
+  float4 bb[FN];
+  if (c < c1) {
+    body(c, acc1, acc0);
+    load_prm((c - c0) % 3, bb);
+    load_res(c);
+    epilogue(c, bb, acc1);
+  } else {
+    load_prm((c1 - 1 - c0) % 3, bb);
+    load_res(c1 - 1);
+    epilogue(c1 - 1, bb, acc0);
+  }
+}
+
 // ---------------------------------------------------------------- host side
 static bool g_force_regstage = getenv("LS_GEMM_REGSTAGE") != nullptr;
 static int g_force_tile = 0, g_force_split = 0, g_ablate = 0, g_bk = 64;
@@ -1202,6 +1422,53 @@ static TileCfg pick_tile(long M, int N, int ktiles, bool allow_split, bool big_o
     }
   }
   return best;
+}
+
+// ---- row-block GEMM dispatch (gemm_rowblock_kernel)
+static bool g_rowblock = getenv("LS_GEMM_NO_ROWBLOCK") == nullptr;
+
+static bool rowblock_ok(const ls_conv_desc* d, const ConvArgs& a) {
+  if (!g_rowblock || g_force_tile || g_force_regstage || d->ksize != 1 || a.C2 || a.aff_scale) return false;
+  if (a.Cin != 320 || a.K != 320 || a.M % 256 || a.N % 64 || a.split != 1 || a.y_f32) return false;
+  if (a.act != LS_ACT_NONE && a.act != LS_ACT_GEGLU) return false;
+  if (a.ldy % 4 || (a.res && a.ldr % 4) || (a.rowvec && (a.rowvec_ld % 4 || a.rows_per_vec % 256))) return false;
+  if (((uintptr_t)a.y | (uintptr_t)a.res) & 7) return false;  // 8-B row pieces
+  return (((uintptr_t)a.x1 | (uintptr_t)a.bias | (uintptr_t)a.ln_cs | (uintptr_t)a.rowvec) & 15) == 0;
+}
+
+// FN = 2 (32-column chunks): the FN = 4 variant needs > 256 VGPRs and spills, and a
+// spill's scratch traffic would break the kernel's counted vmcnt waits.
+template <int FLAGS>
+static void launch_rowblock1(const ConvArgs& a, int grid, hipStream_t s) {
+  constexpr int KT = 10, FN = 2;
+  const size_t shm = (size_t)3 * (16 * FN * (KT / 2) * 8 + 48) * 16;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_rowblock_kernel<KT, FN, FLAGS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    attr = true;
+  }
+  gemm_rowblock_kernel<KT, FN, FLAGS><<<grid, 512, shm, s>>>(a);
+}
+
+// returns false when no instance matches (the caller then uses the tiled kernels)
+static bool launch_rowblock(ConvArgs& a, hipStream_t s) {
+  const int flags = (a.ln_mr ? RB_LN : 0) | (a.res ? RB_RES : 0) | (a.rowvec ? RB_RV : 0) |
+                    (a.act == LS_ACT_GEGLU ? RB_GEGLU : 0);
+  const int ntm = a.M / 256, nch = a.N / 32;
+  a.ntm = ntm;
+  a.ntn = std::max(1, std::min(nch, (256 + ntm - 1) / ntm));
+  const int grid = ntm * a.ntn;
+  switch (flags) {
+    case 0: launch_rowblock1<0>(a, grid, s); return true;
+    case RB_LN: launch_rowblock1<RB_LN>(a, grid, s); return true;
+    case RB_LN | RB_RV: launch_rowblock1<RB_LN | RB_RV>(a, grid, s); return true;
+    case RB_RES: launch_rowblock1<RB_RES>(a, grid, s); return true;
+    case RB_LN | RB_RES: launch_rowblock1<RB_LN | RB_RES>(a, grid, s); return true;
+    case RB_LN | RB_GEGLU: launch_rowblock1<RB_LN | RB_GEGLU>(a, grid, s); return true;
+    case RB_GEGLU: launch_rowblock1<RB_GEGLU>(a, grid, s); return true;
+    default: return false;
+  }
 }
 
 // epilogue variant of a launch (see store_tile)
@@ -1363,6 +1630,7 @@ extern "C" int ls_set_tuning(int32_t key, int32_t value) {
     case 3: g_force_split = value; return LS_OK;
     case 4: g_ablate = value; return LS_OK;
     case 5: if (value != 32 && value != 64) return fail(LS_ERR_INVALID, "BK 32 or 64"); g_bk = value; return LS_OK;
+    case 6: g_rowblock = value != 0; return LS_OK;
     default: return fail(LS_ERR_INVALID, "ls_set_tuning: unknown key");
   }
 }
@@ -1410,6 +1678,7 @@ extern "C" int ls_conv2d(const ls_conv_desc* d, void* stream) {
     if (split > 1) a.partial = (float*)d->workspace;
   }
   hipStream_t s = (hipStream_t)stream;
+  if (rowblock_ok(d, a) && launch_rowblock(a, s)) return check_launch("gemm_rowblock_kernel");
   const bool tapu = (d->ksize == 3) && (a.Cin % 64 == 0);
   const int grid = a.ntm * a.ntn * a.split;
   if (t.bm == 257 && !a.aff_scale && !g_force_regstage && (d->ksize == 1 || tapu)) {  // phased 256x256

@@ -52,6 +52,20 @@ def run():
             ts.append(e0.elapsed_time(e1) / 5)
         t = statistics.median(ts)
         print(f"{os.environ.get('LS_ATTN_V1', 'v2'):3s} {name:18s} {t*1e3:9.1f} us {flops/t/1e9:8.1f} TF/s")
+        if kind != "temporal":  # torch SDPA (vendor flash attention) on the same problem, (B, H, N, d)
+            qt = torch.randn(n, heads, N, d, device="cuda", dtype=torch.bfloat16)
+            kt = torch.randn(n, heads, Nk, d, device="cuda", dtype=torch.bfloat16)
+            vt = torch.randn(n, heads, Nk, d, device="cuda", dtype=torch.bfloat16)
+            sd = lambda: torch.nn.functional.scaled_dot_product_attention(qt, kt, vt)
+            sd()
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(10):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(); sd(); e1.record(); torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            t = statistics.median(ts)
+            print(f"sdp {name:18s} {t*1e3:9.1f} us {flops/t/1e9:8.1f} TF/s")
 
 
 run()

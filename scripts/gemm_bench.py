@@ -15,7 +15,7 @@ SHAPES = [  # (name, n_img, H, Cin, Cout, ksize, act)
     ("ff2_0 1280->320", 16, 32, 1280, 320, 1, 0), ("out0 320->320", 16, 32, 320, 320, 1, 0),
     ("geglu1 640->5120", 16, 16, 640, 5120, 1, 1), ("ff2_1 2560->640", 16, 16, 2560, 640, 1, 0),
     ("geglu2 1280->10240", 16, 8, 1280, 10240, 1, 1), ("ff2_2 5120->1280", 16, 8, 5120, 1280, 1, 0),
-    ("qkv2 1280->3840", 16, 8, 1280, 3840, 1, 0), ("vae conv 128 256^2", 16, 256, 128, 128, 3, 0),
+    ("qkv2 1280->3840", 16, 8, 1280, 3840, 1, 0), ("plain0 320->2560", 16, 32, 320, 2560, 1, 0), ("vae conv 128 256^2", 16, 256, 128, 128, 3, 0),
     ("vae conv 512 32^2", 16, 32, 512, 512, 3, 0),
 ]
 
@@ -89,5 +89,6 @@ if __name__ == "__main__":
         lib.ls_set_tuning(4, ab)
         lib.ls_set_tuning(5, 32 if "bk32" in parts else 64)
         lib.ls_set_tuning(2, tile[0] if tile else 0)
+        lib.ls_set_tuning(6, 0 if "norb" in parts else 1)
         TORCH_REF = "torch" in parts
         run(arg, scale=int(sc or 1))

@@ -2,7 +2,9 @@
 -Rpass-analysis=kernel-resource-usage remarks.  usage: python scripts/kres.py file.hip"""
 import re, subprocess, sys
 src = sys.argv[1]
-r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-munsafe-fp-atomics", "-c", src,
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+from latentsync_amd.build import FLAGS  # noqa: E402
+r = subprocess.run(["/opt/rocm/bin/hipcc"] + FLAGS + ["-c", src,
                     "-o", "/tmp/_kres.o", "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True)
 cur = None
 rows = []

@@ -1,0 +1,10 @@
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -x -q -k "rowblock or layernorm_folded or gemm_tiles or linear" --timeout 120 --timeout-method thread > gpurun_out/p9_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/p9_tests.log; [ $rc -ne 0 ] && exit $rc
+
+rc=$?; tail -3 gpurun_out/p9_tests.log; [ $rc -ne 0 ] && exit $rc
+GEMM_EPI=ln GEMM_ONLY=qkv0,geglu0,out0 timeout -k 10 300 python -u scripts/gemm_bench.py dma@8 dma+norb@8 > gpurun_out/p9_gemm.log 2>&1 || exit 1
+GEMM_EPI=res GEMM_ONLY=out0 timeout -k 10 300 python -u scripts/gemm_bench.py dma@8 dma+norb@8 >> gpurun_out/p9_gemm.log 2>&1 || exit 1
+timeout -k 10 300 python -u scripts/step_calls.py 8 > gpurun_out/p9_calls.log 2>&1

@@ -322,3 +322,56 @@ def test_layernorm_folded_linear(gpu, geglu, pe):
     else:
         y = ops.linear(xd, pk, ln_stats=st, rowvec=rv)
     assert rel_err(y.float().cpu(), y_ref) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,case", [(512, 960, "bias"), (65536, 320, "res"), (4096, 320, "nobias_res_scale"),
+                                      (65536, 1024, "geglu"), (8192, 2560, "ln_geglu"), (65536, 960, "ln_rv")])
+def test_rowblock_gemm(gpu, M, N, case):
+    """The row-block short-K kernel (K = 320, A rows in registers, transposed MFMA,
+    register epilogue) for every epilogue flag combination, on N-split grids (small M)
+    and the full chunk loop (odd / even chunk counts) -- checked against fp32 on the
+    first and last 256 rows, and against the tiled kernel (rowblock off) on all rows.
+    Tolerance 1e-2 (bf16 out)."""
+    from latentsync_amd import _lib
+    lib = _lib.load()
+    K, S, Fr = 320, 1024, 16
+    x = bf(rnd(M, K, seed=90) * (2 if "ln" in case else 1) + (3 if "ln" in case else 0))
+    geglu = "geglu" in case
+    w = rnd(N, K, seed=91, scale=1 / math.sqrt(K))
+    b = None if "nobias" in case else rnd(N, seed=92, scale=0.1)
+    xd = x.to(torch.bfloat16).to(DEV)
+    kw, scale = {}, 1.0
+    rows = torch.cat([torch.arange(256), torch.arange(M - 256, M)])
+    if "ln" in case:
+        from latentsync_amd.unet import _Dev
+        gamma, beta = 1 + 0.1 * rnd(K, seed=93), 0.1 * rnd(K, seed=94)
+        pe_t = rnd(24, K, seed=95) if "rv" in case else None
+        pk = _Dev({}, DEV).packed_ln(w, b, (gamma, beta), geglu=geglu, pe=pe_t)
+        kw["ln_stats"] = ops.row_stats(xd)
+        t = F.layer_norm(x[rows], (K,), gamma, beta, 1e-5)
+        if pe_t is not None:
+            kw["rowvec"] = (pk.pe_rows, S, pk.pe_rows.shape[1], Fr)
+            t = t + pe_t[(rows // S) % Fr]
+    else:
+        pk = packed(w, b, 1, geglu=geglu)
+        t = x[rows]
+    ref = t @ w.T + (b if b is not None else 0)
+    if "res" in case:
+        res = bf(rnd(M, N, seed=96))
+        kw["res"] = res.to(torch.bfloat16).to(DEV)
+        ref = ref + res[rows]
+    if "scale" in case:
+        scale = 0.5
+        ref = ref * scale
+    if geglu:
+        h, g = ref.chunk(2, -1)
+        ref = h * F.gelu(g)
+        kw["act"] = ops.ACT_GEGLU
+    y = ops.linear(xd, pk, out_scale=scale, **kw)
+    lib.ls_set_tuning(6, 0)
+    try:
+        y_tiled = ops.linear(xd, pk, out_scale=scale, **kw)
+    finally:
+        lib.ls_set_tuning(6, 1)
+    assert rel_err(y.float().cpu()[rows], ref) < 1e-2
+    assert rel_err(y.float(), y_tiled.float()) < 1e-2
