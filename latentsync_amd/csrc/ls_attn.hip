@@ -402,6 +402,134 @@ static int launch_attn(const AttnArgs& a, int batch, int heads, hipStream_t s) {
   return check_launch("attn_kernel");
 }
 
+
+// ------------------------------------------------- short sequences (temporal)
+// VersatileAttention over the 16 frames of a window (motion_module.py:203-239) is
+// 16 queries x 16 keys per (pixel, head): far too small for MFMA tiles, and the
+// flash kernel above spent a 256-thread block per (pixel, head) re-reading 80-B
+// head slices.  Here a block owns NB whole (pixel) sequences -- all heads, i.e.
+// full contiguous C-channel rows of K and V, read once with 16-B loads -- stages
+// them row-major in LDS, and every thread computes one (sequence, head, query):
+// QK^T with packed-bf16 dot products (v_dot2_f32_bf16, fp32 accumulation), fp32
+// softmax, P V as fp32 FMAs over the 16 keys.  TS threads split the head dim
+// (partial dots summed with lane shuffles, D/TS output dims each).  All LDS reads
+// are broadcasts within a (sequence, head) lane group.  HBM bound: q, k, v read
+// once, o written once.
+// Host contract: nq == nk <= 16, heads contiguous (q/k/v/o head stride == D),
+// D / TS == 40, heads * 16 * TS divides the block (256 or 512), 16-B aligned rows.
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+template <int D, int TS, int NT>
+__global__ void __launch_bounds__(NT, 4) attn_seq_kernel(AttnArgs a, int H, int nbatch) {
+  constexpr int DT = D / TS;                  // head dims per thread (40)
+  constexpr int DC = DT / 8;                  // 16-B chunks per thread slice
+  const int C = H * D;
+  const int F = a.nk;
+  const int NB = NT / (H * 16 * TS);          // sequences per block
+  extern __shared__ __attribute__((aligned(16))) u16 sm[];
+  u16* Ks = sm;                               // [NB][16][C]
+  u16* Vs = sm + NB * 16 * C;                 // [NB][16][C]
+  const int tid = threadIdx.x;
+  const int bz0 = blockIdx.x * NB;
+
+  // ---- stage K and V rows of the block's sequences (zero rows past F / nbatch)
+  const int cpr = C / 8;  // 16-B chunks per row
+  for (int q = tid; q < NB * 16 * cpr; q += NT) {
+    const int nb = q / (16 * cpr), r = q - nb * 16 * cpr;
+    const int j = r / cpr, c8 = (r - j * cpr) * 8;
+    const int bz = bz0 + nb;
+    uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+    if (bz < nbatch && j < F) {
+      const long b1 = bz / a.z2, b2 = bz - b1 * a.z2;
+      kv = *(const uint4*)(a.k + b1 * a.k_sb1 + b2 * a.k_sb2 + j * a.k_si + c8);
+      vv = *(const uint4*)(a.v + b1 * a.v_sb1 + b2 * a.v_sb2 + j * a.v_si + c8);
+    }
+    *(uint4*)(Ks + (nb * 16 + j) * C + c8) = kv;
+    *(uint4*)(Vs + (nb * 16 + j) * C + c8) = vv;
+  }
+
+  // ---- this thread's item: lane = query * TS + ts inside a 16*TS-lane (sequence, head) group
+  const int grp = tid / (16 * TS), in = tid - grp * 16 * TS;
+  const int qi = in / TS, ts = in - qi * TS;
+  const int nb = grp / H, h = grp - nb * H;
+  const int bz = bz0 + nb;
+  const bool live = bz < nbatch && qi < F;
+  const long b1 = bz / a.z2, b2 = bz - b1 * a.z2;
+  bf16x2 qv[DT / 2];
+  {
+    const u16* qp = a.q + b1 * a.q_sb1 + b2 * a.q_sb2 + (long)qi * a.q_si + (long)h * a.q_sh + ts * DT;
+#pragma unroll
+    for (int c = 0; c < DC; ++c) {
+      const uint4 u = live ? *(const uint4*)(qp + c * 8) : make_uint4(0, 0, 0, 0);
+      qv[4 * c + 0] = __builtin_bit_cast(bf16x2, u.x); qv[4 * c + 1] = __builtin_bit_cast(bf16x2, u.y);
+      qv[4 * c + 2] = __builtin_bit_cast(bf16x2, u.z); qv[4 * c + 3] = __builtin_bit_cast(bf16x2, u.w);
+    }
+  }
+  __syncthreads();
+
+  // ---- scores (log2 domain), softmax over the F keys
+  const int off = nb * 16 * C + h * D + ts * DT;
+  float sc[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < DC; ++c) {
+      const uint4 u = *(const uint4*)(Ks + off + j * C + c * 8);
+      acc = __builtin_amdgcn_fdot2_f32_bf16(qv[4 * c + 0], __builtin_bit_cast(bf16x2, u.x), acc, false);
+      acc = __builtin_amdgcn_fdot2_f32_bf16(qv[4 * c + 1], __builtin_bit_cast(bf16x2, u.y), acc, false);
+      acc = __builtin_amdgcn_fdot2_f32_bf16(qv[4 * c + 2], __builtin_bit_cast(bf16x2, u.z), acc, false);
+      acc = __builtin_amdgcn_fdot2_f32_bf16(qv[4 * c + 3], __builtin_bit_cast(bf16x2, u.w), acc, false);
+    }
+#pragma unroll
+    for (int o = 1; o < TS; o <<= 1) acc += __shfl_xor(acc, o, 64);
+    sc[j] = j < F ? acc * a.scale_log2 : -INFINITY;
+  }
+  float m = sc[0];
+#pragma unroll
+  for (int j = 1; j < 16; ++j) m = fmaxf(m, sc[j]);
+  float l = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    // probabilities rounded to bf16 as the PV operand of a bf16 SDPA would be
+    sc[j] = (float)(__bf16)exp2f(sc[j] - m);
+    l += sc[j];
+  }
+  const float inv = 1.f / l;
+
+  // ---- O[dims ts*DT .. +DT) = sum_j p_j V[j][dim] / l, one 8-dim chunk at a time
+  u16* op = a.o + b1 * a.o_sb1 + b2 * a.o_sb2 + (long)qi * a.o_si + (long)h * a.o_sh + ts * DT;
+#pragma unroll
+  for (int c = 0; c < DC; ++c) {
+    float o8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      float v8[8];
+      unpack8(*(const uint4*)(Vs + off + j * C + c * 8), v8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o8[e] = fmaf(sc[j], v8[e], o8[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o8[e] *= inv;
+    if (live) *(uint4*)(op + c * 8) = pack8(o8);
+  }
+}
+
+template <int D, int TS, int NT>
+static int launch_seq(const AttnArgs& a, int batch, int heads, hipStream_t s) {
+  const int nb = NT / (heads * 16 * TS);
+  const int C = heads * D;
+  const size_t shm = (size_t)nb * 16 * C * 2 * sizeof(u16);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)attn_seq_kernel<D, TS, NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)shm);
+    attr_set = true;
+  }
+  attn_seq_kernel<D, TS, NT><<<cdiv(batch, nb), NT, shm, s>>>(a, heads, batch);
+  return check_launch("attn_seq_kernel");
+}
+
 }  // namespace ls
 
 using namespace ls;
@@ -424,6 +552,24 @@ extern "C" int ls_attention(const ls_attn_desc* d, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const bool small = d->nk <= 32;
   const int D = d->head_dim;
+  // short sequences (the temporal attention over a window's frames): whole-row kernel
+  {
+    const int H = d->heads, TS = D / 40;
+    const bool heads_packed = d->q_sh == D && d->k_sh == D && d->v_sh == D && d->o_sh == D;
+    const bool aligned = d->q_si % 8 == 0 && d->k_si % 8 == 0 && d->v_si % 8 == 0 && d->o_si % 8 == 0 &&
+                         d->q_sb1 % 8 == 0 && d->q_sb2 % 8 == 0 && d->k_sb1 % 8 == 0 && d->k_sb2 % 8 == 0 &&
+                         d->v_sb1 % 8 == 0 && d->v_sb2 % 8 == 0 && d->o_sb1 % 8 == 0 && d->o_sb2 % 8 == 0 &&
+                         (((uintptr_t)d->q | (uintptr_t)d->k | (uintptr_t)d->v | (uintptr_t)d->o) & 15) == 0;
+    if (!g_attn_v1 && d->nq == d->nk && d->nk <= 16 && heads_packed && aligned && D % 40 == 0 &&
+        (TS == 1 || TS == 2 || TS == 4) && H * 16 * TS <= 512 && 512 % (H * 16 * TS) == 0) {
+      // 256-thread blocks (several per CU desynchronise the load and compute phases)
+      // wherever one (sequence, head) set fits
+      const bool small_blk = H * 16 * TS <= 256 && 256 % (H * 16 * TS) == 0;
+      if (D == 40) return small_blk ? launch_seq<40, 1, 256>(a, d->batch, H, s) : launch_seq<40, 1, 512>(a, d->batch, H, s);
+      if (D == 80) return small_blk ? launch_seq<80, 2, 256>(a, d->batch, H, s) : launch_seq<80, 2, 512>(a, d->batch, H, s);
+      if (D == 160) return launch_seq<160, 4, 512>(a, d->batch, H, s);
+    }
+  }
   if (!small && D % 8 == 0 && D <= 160 && !g_attn_v1) {
     // ND = ceil(D / 16) output fragments, KC = ceil(D / 32) contraction chunks
     switch ((D + 15) / 16) {

@@ -167,11 +167,13 @@ def test_attention_spatial(gpu, n, N, Nk, heads, d):
     assert rel_err(o.float().cpu(), ref) < 1.5e-2
 
 
-@pytest.mark.parametrize("C", [320, 1280])
-def test_attention_temporal_strided(gpu, C):
+@pytest.mark.parametrize("C,Fr,S", [(320, 16, 16), (640, 16, 16), (1280, 16, 16), (320, 12, 15), (640, 7, 9),
+                                    (1280, 16, 3)])
+def test_attention_temporal_strided(gpu, C, Fr, S):
     """VersatileAttention: '(b f) s c -> (b s) f c' read straight from the fused
-    q|k|v rows (motion_module.py:265, 300)."""
-    B, Fr, S, heads = 2, 16, 16, 8
+    q|k|v rows (motion_module.py:265, 300) -- the short-sequence kernel, incl.
+    fewer frames than 16 and (pixel) batches that do not fill its blocks."""
+    B, heads = 2, 8
     d = C // heads
     qkv = bf(rnd(B * Fr * S, 3 * C, seed=60))
     q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
