@@ -145,11 +145,15 @@ gn_stats_kernel(const u16* __restrict__ x1, const u16* __restrict__ x2, int C1, 
 }
 
 static int gn_nsplit(int n_samples, long pps, int C) {
-  // ~8 pixel rows per thread (one batch of 8 loads in flight each), <= ~4096 blocks
+  // Every block adds its per-group fp64 partials into one accumulator per (sample,
+  // group) with memory-side atomics, which serialise per address: aim for ~512
+  // blocks in total (2 per CU keep ~12 MB of loads in flight), i.e. as many pixel
+  // rows per thread as that allows (>= 8, one batch of 8 loads).  Measured on the
+  // UNet / VAE shapes this halves the 32x32 stats pass (59 -> 28 us, 8 windows).
   const int CC = C / 8;
   const int R = CC <= GN_THREADS ? GN_THREADS / CC : 1;
-  long ns = pps / (8L * R);
-  ns = std::min<long>(ns, std::max<long>(1, cdiv(4096, n_samples)));
+  long ns = cdiv(512, n_samples);
+  ns = std::min<long>(ns, pps / (8L * R));
   return (int)std::max<long>(1, std::min<long>(ns, 4096));
 }
 
