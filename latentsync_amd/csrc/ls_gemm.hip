@@ -1270,9 +1270,10 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
   asm volatile("" ::: "memory");
 
   f32x4 acc0[FM][FN], acc1[FM][FN];
-  uint2 rs[FM][FN];
+  uint2 rsA[FM][FN], rsB[FM][FN];  // residual of the chunk being computed / of the one in its epilogue
+  constexpr int NRES = RES ? FM * FN : 0;
 
-  auto load_res = [&](int c) {
+  auto load_res = [&](int c, uint2 (&rs)[FM][FN]) {
     if (!RES) return;
     const int nb = c * BN + 4 * lg;
 #pragma unroll
@@ -1294,7 +1295,7 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
       }
     }
   };
-  auto epilogue = [&](int c, const float4 (&bb)[FN], f32x4 (&acc)[FM][FN]) {
+  auto epilogue = [&](int c, const float4 (&bb)[FN], f32x4 (&acc)[FM][FN], const uint2 (&rs)[FM][FN]) {
     const int nb = c * BN + 4 * lg;  // packed column of fragment j: nb + 16 j
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
@@ -1355,37 +1356,39 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
   // 3-stage ring: chunk c computes from stage c%3 while chunk c-1's parameters stay in
   // (c-1)%3 for its epilogue and chunk c+1 lands in (c+1)%3.  Past the last chunk the DMA
   // re-loads the last chunk into the spare stage, so the steady-state body is branch-free.
-  auto body = [&](int c, f32x4 (&acc)[FM][FN], f32x4 (&prev)[FM][FN]) {
+  // The residual of chunk c is loaded a whole chunk ahead of its epilogue, younger than
+  // the DMA, so the end-of-chunk wait (DMA landed) leaves it in flight.
+  auto body = [&](int c, f32x4 (&acc)[FM][FN], f32x4 (&prev)[FM][FN], uint2 (&rs_load)[FM][FN],
+                  uint2 (&rs_use)[FM][FN]) {
     const int st = (c - c0) % 3;
     float4 bb[FN];
     load_prm(st == 0 ? 2 : st - 1, bb);
-    load_res(c - 1);                                         // older than the DMA: waited on alone
     issue(min(c + 1, c1 - 1), st == 2 ? 0 : st + 1);
+    load_res(c, rs_load);
     mfma_chunk(st, acc);
-    epilogue(c - 1, bb, prev);
-    wait_vm<NSTORE>();                                       // the DMA (older than the stores) landed
+    epilogue(c - 1, bb, prev, rs_use);
+    wait_vm<NSTORE + NRES>();                                // the DMA (older than both) landed
     sync();
   };
   // first chunk: no epilogue
   issue(min(c0 + 1, c1 - 1), 1);
+  load_res(c0, rsA);
   mfma_chunk(0, acc0);
-  wait_vm<0>();
+  wait_vm<NRES>();
   sync();
   int c = c0 + 1;
   for (; c + 1 < c1; c += 2) {
-    body(c, acc1, acc0);
-    body(c + 1, acc0, acc1);
+    body(c, acc1, acc0, rsB, rsA);
+    body(c + 1, acc0, acc1, rsA, rsB);
   }
   float4 bb[FN];
   if (c < c1) {
-    body(c, acc1, acc0);
+    body(c, acc1, acc0, rsB, rsA);
     load_prm((c - c0) % 3, bb);
-    load_res(c);
-    epilogue(c, bb, acc1);
+    epilogue(c, bb, acc1, rsB);
   } else {
     load_prm((c1 - 1 - c0) % 3, bb);
-    load_res(c1 - 1);
-    epilogue(c1 - 1, bb, acc0);
+    epilogue(c1 - 1, bb, acc0, rsA);
   }
 }
 
