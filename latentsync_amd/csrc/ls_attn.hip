@@ -10,6 +10,8 @@
 // O^T = V^T P^T, with no LDS round trip: the MFMA's k index is permuted
 // identically on both operands (keys 32c+4h+j and 32c+16+4h+j for lane group h),
 // and V^T comes from the row-major V tile through ds_read_b64_tr_b16.
+#include <type_traits>
+
 #include "ls_common.h"
 
 typedef short v4i16 __attribute__((ext_vector_type(4)));
@@ -119,14 +121,14 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
     mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
     const float mn = fmaxf(m, mt);
-    const float alpha = exp2f(m - mn);
+    const float alpha = fast_exp2(m - mn);
     m = mn;
     float ps = 0.f;
 #pragma unroll
     for (int f = 0; f < NKF; ++f)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(s[f][r] - mn);
+        const float p = fast_exp2(s[f][r] - mn);
         s[f][r] = p;
         ps += p;
       }
@@ -182,7 +184,7 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
 typedef float f2v __attribute__((ext_vector_type(2)));
 
 template <int KC, int ND>
-__global__ void __launch_bounds__(256) attn2_kernel(AttnArgs a) {
+__global__ void __launch_bounds__(256, KC >= 5 ? 1 : 2) attn2_kernel(AttnArgs a) {
   constexpr int DP = KC * 32;
   constexpr int KT = 64;
   constexpr int PITCH = DP + 8;
@@ -261,7 +263,9 @@ __global__ void __launch_bounds__(256) attn2_kernel(AttnArgs a) {
   __syncthreads();  // padding zeroed
   lstore(0);
   const int ntile = (a.nk + KT - 1) / KT;
-  for (int t = 0; t < ntile; ++t) {
+  // one 64-key tile; PARTIAL (the last tile when nk % 64 != 0) masks keys >= nk
+  auto tile = [&](int t, auto partial_tag) {
+    constexpr bool PARTIAL = decltype(partial_tag)::value;
     const int t0 = t * KT;
     __syncthreads();  // tile t visible; buffer t^1 free
     if (t + 1 < ntile) gload(t0 + KT);
@@ -280,40 +284,38 @@ __global__ void __launch_bounds__(256) attn2_kernel(AttnArgs a) {
         s[1][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[1][kc], s[1][f], 0, 0, 0);
       }
     }
-    const bool full = t0 + KT <= a.nk;
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
-      if (!full) {
+      if (PARTIAL) {
 #pragma unroll
         for (int f = 0; f < 4; ++f)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             if (t0 + 16 * f + 4 * lg + r >= a.nk) s[g][f][r] = -INFINITY;
       }
-      float mt = fmaxf(fmaxf(s[g][0][0], s[g][0][1]), fmaxf(s[g][0][2], s[g][0][3]));
+      // running max: IEEE maximum (v_maximum3_f32), no NaN-canonicalising self-max per input
+      float mt = __builtin_elementwise_maximum(__builtin_elementwise_maximum(s[g][0][0], s[g][0][1]),
+                                               __builtin_elementwise_maximum(s[g][0][2], s[g][0][3]));
 #pragma unroll
       for (int f = 1; f < 4; ++f)
-        mt = fmaxf(mt, fmaxf(fmaxf(s[g][f][0], s[g][f][1]), fmaxf(s[g][f][2], s[g][f][3])));
-      mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-      const float mn = fmaxf(m[g], mt * c2);
-      const float alpha = exp2f(m[g] - mn);
+        mt = __builtin_elementwise_maximum(
+            mt, __builtin_elementwise_maximum(__builtin_elementwise_maximum(s[g][f][0], s[g][f][1]),
+                                              __builtin_elementwise_maximum(s[g][f][2], s[g][f][3])));
+      mt = __builtin_elementwise_maximum(mt, __shfl_xor(mt, 16, 64));
+      mt = __builtin_elementwise_maximum(mt, __shfl_xor(mt, 32, 64));
+      const float mn = __builtin_elementwise_maximum(m[g], mt * c2);
+      const float alpha = fast_exp2(m[g] - mn);
       m[g] = mn;
-      f2v ps = {0.f, 0.f};
-      const f2v cc = {c2, c2}, nm = {-mn, -mn};
+      float ps = 0.f;
 #pragma unroll
       for (int f = 0; f < 4; ++f)
 #pragma unroll
-        for (int r = 0; r < 4; r += 2) {
-          f2v x = {s[g][f][r], s[g][f][r + 1]};
-          x = x * cc + nm;
-          x.x = exp2f(x.x);
-          x.y = exp2f(x.y);
-          s[g][f][r] = x.x;
-          s[g][f][r + 1] = x.y;
-          ps += x;
+        for (int r = 0; r < 4; ++r) {
+          const float p = fast_exp2(fmaf(s[g][f][r], c2, -mn));
+          s[g][f][r] = p;
+          ps += p;
         }
-      l[g] = l[g] * alpha + ps.x + ps.y;
+      l[g] = fmaf(l[g], alpha, ps);
 #pragma unroll
       for (int i = 0; i < ND; ++i) oacc[g][i] *= alpha;
     }
@@ -342,7 +344,10 @@ __global__ void __launch_bounds__(256) attn2_kernel(AttnArgs a) {
       }
     }
     if (t + 1 < ntile) lstore((t + 1) & 1);
-  }
+  };
+  const int nfull = a.nk / KT;
+  for (int t = 0; t < nfull; ++t) tile(t, std::false_type{});
+  if (nfull < ntile) tile(nfull, std::true_type{});
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
     float lt = l[g];
@@ -492,7 +497,7 @@ __global__ void __launch_bounds__(NT, 4) attn_seq_kernel(AttnArgs a, int H, int 
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     // probabilities rounded to bf16 as the PV operand of a bf16 SDPA would be
-    sc[j] = (float)(__bf16)exp2f(sc[j] - m);
+    sc[j] = (float)(__bf16)fast_exp2(sc[j] - m);
     l += sc[j];
   }
   const float inv = 1.f / l;

@@ -40,6 +40,12 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
 }
 
+// 2^x as the bare v_exp_f32: exp2f() wraps it in a denormal-range fix-up (compare,
+// two selects and a v_ldexp around every call -- 5 VALU ops where the softmax and
+// GELU need 1).  Results below 2^-126 flush to 0, which every caller tolerates
+// (softmax terms, erf tails).
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 // x * sigmoid(x) with a hardware reciprocal (1-2 ulp; outputs are bf16)
 __device__ __forceinline__ float silu(float x) { return x * __frcp_rn(1.0f + __expf(-x)); }
 
@@ -51,7 +57,7 @@ __device__ __forceinline__ float gelu_erf(float x) {
   const float t = __frcp_rn(fmaf(0.3275911f, z, 1.0f));
   const float p = t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f),
                            0.254829592f);
-  const float e = exp2f(-z * z * 1.4426950408889634f);
+  const float e = fast_exp2(-z * z * 1.4426950408889634f);
   const float erfz = fmaf(-p, e, 1.0f);
   return 0.5f * x * (1.0f + copysignf(erfz, x));
 }

@@ -15,7 +15,10 @@ CASES = [  # name, batch(frames), tokens, keys, heads, d, kind
 
 
 def run():
+    only = os.environ.get("ATTN_ONLY")
     for name, n, N, Nk, heads, d, kind in CASES:
+        if only and only not in name:
+            continue
         C = heads * d
         if kind == "temporal":
             Fr, S = 16, N
@@ -52,7 +55,7 @@ def run():
             ts.append(e0.elapsed_time(e1) / 5)
         t = statistics.median(ts)
         print(f"{os.environ.get('LS_ATTN_V1', 'v2'):3s} {name:18s} {t*1e3:9.1f} us {flops/t/1e9:8.1f} TF/s")
-        if kind != "temporal":  # torch SDPA (vendor flash attention) on the same problem, (B, H, N, d)
+        if kind != "temporal" and not os.environ.get("NO_SDPA"):  # torch SDPA (vendor flash attention) on the same problem, (B, H, N, d)
             qt = torch.randn(n, heads, N, d, device="cuda", dtype=torch.bfloat16)
             kt = torch.randn(n, heads, Nk, d, device="cuda", dtype=torch.bfloat16)
             vt = torch.randn(n, heads, Nk, d, device="cuda", dtype=torch.bfloat16)
