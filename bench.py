@@ -295,7 +295,7 @@ def main():
             "single_window": single,
             "window_mfma_frac": round(tf_per_frame * value / world / PEAK_BF16_TF, 4),
             "roofline": {"bound": "mfma",
-                         "kernel": "conv_gemm family: every ls_conv2d call of one UNet fwd (conv_gemm_* GEMM + split-K reduce)",
+                         "kernel": "conv_gemm family: every ls_conv2d call of one UNet fwd (conv_gemm_* tiled / gemm_rowblock GEMM + split-K reduce)",
                          "achieved": round(probe["tflops"], 2), "peak": PEAK_BF16_TF, "unit": "TFLOP/s",
                          "frac": round(probe["tflops"] / PEAK_BF16_TF, 4), "traffic": traffic_per_call(),
                          "traffic_unit": "HBM bytes per ls_conv2d call (rocprofv3 PMC, profiles/pmc_traffic.json)",

@@ -1,2 +1,5 @@
+# Round-end GPU evidence: gpu tests -> bench -> rocprofv3 kernel stats -> two PMC passes.
+# usage: bash scripts/gpu_round.sh TAG
 set -o pipefail
-bash scripts/gpu_full.sh r1d && bash scripts/pmc_pass.sh r1d
+tag=${1:-r1e}
+bash scripts/gpu_full.sh $tag && bash scripts/pmc_pass.sh $tag
