@@ -586,11 +586,12 @@ __device__ __forceinline__ int swz_bk(int row, int c) {
 }
 
 template <int BM, int BN, int WM, int WN, int KS, bool TAPU, int NST, int BK, int EPI>
-__global__ void __launch_bounds__(256) conv_gemm_dma_kernel(ConvArgs a) {
+__global__ void __launch_bounds__(WM * WN * 64) conv_gemm_dma_kernel(ConvArgs a) {
+  constexpr int NT = WM * WN * 64;                    // 256 (4 waves) or 512 (8 waves, 256-row tiles)
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int FM = WTM / 16, FN = WTN / 16;
   constexpr int CPR = BK / 8;                         // 16-B chunks per row
-  constexpr int AI = BM * CPR / 256, BI = BN * CPR / 256;  // DMA wave-instructions per wave per K-tile
+  constexpr int AI = BM * CPR / NT, BI = BN * CPR / NT;  // DMA wave-instructions per wave per K-tile
   constexpr int L = AI + BI;
   constexpr int KSTEPS = BK / 32;
   constexpr int STAGE = (BM + BN) * CPR;              // uint4 per stage
@@ -1493,13 +1494,13 @@ static void launch_dma1(const ConvArgs& a, int grid, hipStream_t s) {
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     attr = true;
   }
-  conv_gemm_dma_kernel<BM, BN, WM, WN, KS, TAPU, NST, BK, EPI><<<grid, 256, shm, s>>>(a);
+  conv_gemm_dma_kernel<BM, BN, WM, WN, KS, TAPU, NST, BK, EPI><<<grid, WM * WN * 64, shm, s>>>(a);
 }
 
 template <int BM, int BN, int WM, int WN, int KS, bool TAPU>
 static void launch_dma(const ConvArgs& a, int grid, hipStream_t s) {
   if constexpr (BN >= 64) {
-    if (g_bk == 32) { launch_dma1<BM, BN, WM, WN, KS, TAPU, 3, 32, EPI_ANY>(a, grid, s); return; }
+    if (g_bk == 32) { launch_dma1<BM, BN, WM, WN, KS, TAPU, 4, 32, EPI_ANY>(a, grid, s); return; }
   }
   switch (epi_kind(a)) {
     case EPI_PLAIN: launch_dma1<BM, BN, WM, WN, KS, TAPU, 2, 64, EPI_PLAIN>(a, grid, s); break;
@@ -1608,11 +1609,11 @@ static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split
   t = pick_tile(M, d->N, a.ktiles, d->split_k <= 0 && d->workspace != nullptr,
                 !d->aff_scale && !g_force_regstage && (d->ksize == 1 || Cin % 64 == 0));
   if (g_force_tile) {
-    static const int tb[10][2] = {{0, 0}, {128, 128}, {128, 64}, {64, 64}, {128, 32}, {256, 256}, {256, 128},
-                                  {257, 256}, {258, 256}, {128, 160}};
+    static const int tb[11][2] = {{0, 0}, {128, 128}, {128, 64}, {64, 64}, {128, 32}, {256, 256}, {256, 128},
+                                  {257, 256}, {258, 256}, {128, 160}, {259, 160}};
     t.bm = tb[g_force_tile][0]; t.bn = tb[g_force_tile][1]; t.split = g_force_split ? g_force_split : 1;
   }
-  a.ntm = cdiv(M, t.bm > 256 ? 256 : t.bm); a.ntn = cdiv(d->N, t.bn);  // 257/258 = 256x256 kernel variants
+  a.ntm = cdiv(M, t.bm > 256 ? 256 : t.bm); a.ntn = cdiv(d->N, t.bn);  // 257/258/259 = 256-row kernel variants
   split = d->split_k > 0 ? d->split_k : t.split;
   split = std::min(split, a.ktiles);
   a.kt_per_split = cdiv(a.ktiles, split);
@@ -1629,7 +1630,7 @@ using namespace ls;
 extern "C" int ls_set_tuning(int32_t key, int32_t value) {
   switch (key) {
     case 1: g_force_regstage = value != 0; return LS_OK;
-    case 2: if (value < 0 || value > 9) return fail(LS_ERR_INVALID, "tile id 0..9"); g_force_tile = value; return LS_OK;
+    case 2: if (value < 0 || value > 10) return fail(LS_ERR_INVALID, "tile id 0..10"); g_force_tile = value; return LS_OK;
     case 3: g_force_split = value; return LS_OK;
     case 4: g_ablate = value; return LS_OK;
     case 5: if (value != 32 && value != 64) return fail(LS_ERR_INVALID, "BK 32 or 64"); g_bk = value; return LS_OK;
@@ -1695,6 +1696,8 @@ extern "C" int ls_conv2d(const ls_conv_desc* d, void* stream) {
     else launch_big<128>(a, d->ksize, tapu, grid, s);
   } else if (t.bm == 128 && t.bn == 128) launch_cfg<128, 128, 2, 2>(a, d->ksize, tapu, grid, s);
   else if (t.bm == 128 && t.bn == 160) launch_cfg<128, 160, 2, 2>(a, d->ksize, tapu, grid, s);
+  else if (t.bm == 259 && t.bn == 160 && d->ksize == 3 && tapu && !a.aff_scale)
+    launch_dma1<256, 160, 4, 2, 3, true, 3, 64, EPI_ANY>(a, grid, s);  // 8-wave 3x3 tile, 3-stage ring
   else if (t.bm == 128 && t.bn == 64) launch_cfg<128, 64, 2, 2>(a, d->ksize, tapu, grid, s);
   else if (t.bm == 128 && t.bn == 32) launch_cfg<128, 32, 4, 1>(a, d->ksize, tapu, grid, s);
   else launch_cfg<64, 64, 2, 2>(a, d->ksize, tapu, grid, s);
