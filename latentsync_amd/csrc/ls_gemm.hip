@@ -1191,13 +1191,15 @@ __global__ void splitk_reduce_kernel(ConvArgs a) {
 // FLAGS: RB_LN LayerNorm fold (ln_rowstats/ln_colsum), RB_RES residual,
 // RB_RV row vector (positional-encoding rows), RB_GEGLU GEGLU epilogue.  With RB_LN the
 // register-resident A rows are normalised in place (the host folds gamma / beta).
-// Host contract (rowblock_ok): ksize 1, no x2 / affine prologue, K = 32*KT = Cin,
-// M % 256 == 0, N % 64 == 0, no split-K, bf16 output with 4-aligned pitches.
+// Host contract (rowblock_ok): ksize 1, no x2 / affine prologue, K = 32*KT = Cin
+// (320 with FM = 2: 256 rows per block; 640 with FM = 1: 128 rows, A still 80 VGPRs),
+// M % BM == 0, N % 64 == 0, no split-K, bf16 output with 4-aligned pitches.
 enum { RB_LN = 1, RB_RES = 2, RB_RV = 4, RB_GEGLU = 8 };
 
-template <int KT, int FN, int FLAGS>
+template <int KT, int FM, int FN, int FLAGS>
 __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
-  constexpr int FM = 2, BN = 16 * FN;
+  constexpr int BN = 16 * FN;
+  constexpr int BM = 8 * 16 * FM;             // rows per workgroup (8 waves x FM fragments of 16)
   constexpr int KTILES = KT / 2;              // 64-wide LDS images per chunk
   constexpr int WIMG = BN * KTILES * 8;       // uint4 of the W images of a chunk
   constexpr int STAGE = WIMG + 48;            // + bias / colsum / row-vector columns (3 x 64 fp32)
@@ -1211,12 +1213,12 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
   const int rb = blockIdx.x / a.ntn, ns = blockIdx.x - rb * a.ntn;
   const int nch = a.N / BN;
   const int c0 = (int)((long)nch * ns / a.ntn), c1 = (int)((long)nch * (ns + 1) / a.ntn);
-  const int mw = rb * 256 + wid * 32;  // this wave's first row
+  const int mw = rb * BM + wid * 16 * FM;  // this wave's first row
 
   // chunk c -> LDS stage: W rows [64c, 64c + 64) x all K as KTILES swizzled 64-wide
   // images, then the chunk's 64 bias, colsum and row-vector values (wave 0).
   // piece q = p * 512 + tid of a chunk's images: image t = q / (8 BN), row (q / 8) % BN, chunk q % 8
-  const long rv_base = RV ? rv_row(a, rb * 256) : 0;  // host: rows_per_vec % 256 == 0
+  const long rv_base = RV ? rv_row(a, rb * BM) : 0;  // host: rows_per_vec % BM == 0
   auto issue = [&](int c, int stage) {
     uint4* dst = lds_dyn + stage * STAGE;
 #pragma unroll
@@ -1430,10 +1432,15 @@ static TileCfg pick_tile(long M, int N, int ktiles, bool allow_split, bool big_o
 
 // ---- row-block GEMM dispatch (gemm_rowblock_kernel)
 static bool g_rowblock = getenv("LS_GEMM_NO_ROWBLOCK") == nullptr;
+static bool g_rowblock640 = getenv("LS_GEMM_NO_ROWBLOCK640") == nullptr;
 
 static bool rowblock_ok(const ls_conv_desc* d, const ConvArgs& a) {
   if (!g_rowblock || g_force_tile || g_force_regstage || d->ksize != 1 || a.C2 || a.aff_scale) return false;
-  if (a.Cin != 320 || a.K != 320 || a.M % 256 || a.N % 64 || a.split != 1 || a.y_f32) return false;
+  // K = 640 only without a residual (the tiled kernel is faster there: 48 vs 53 us at 16x16)
+  if (!((a.Cin == 320 && a.K == 320 && a.M % 256 == 0) ||
+        (g_rowblock640 && a.Cin == 640 && a.K == 640 && a.M % 128 == 0 && !a.res)))
+    return false;
+  if (a.N % 64 || a.split != 1 || a.y_f32) return false;
   if (a.act != LS_ACT_NONE && a.act != LS_ACT_GEGLU) return false;
   if (a.ldy % 4 || (a.res && a.ldr % 4) || (a.rowvec && (a.rowvec_ld % 4 || a.rows_per_vec % 256))) return false;
   if (((uintptr_t)a.y | (uintptr_t)a.res) & 7) return false;  // 8-B row pieces
@@ -1442,24 +1449,31 @@ static bool rowblock_ok(const ls_conv_desc* d, const ConvArgs& a) {
 
 // FN = 2 (32-column chunks): the FN = 4 variant needs > 256 VGPRs and spills, and a
 // spill's scratch traffic would break the kernel's counted vmcnt waits.
-template <int FLAGS>
-static void launch_rowblock1(const ConvArgs& a, int grid, hipStream_t s) {
-  constexpr int KT = 10, FN = 2;
+template <int KT, int FM, int FLAGS>
+static void launch_rowblock2(const ConvArgs& a, int grid, hipStream_t s) {
+  constexpr int FN = 2;
   const size_t shm = (size_t)3 * (16 * FN * (KT / 2) * 8 + 48) * 16;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_rowblock_kernel<KT, FN, FLAGS>,
+    (void)hipFuncSetAttribute((const void*)gemm_rowblock_kernel<KT, FM, FN, FLAGS>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     attr = true;
   }
-  gemm_rowblock_kernel<KT, FN, FLAGS><<<grid, 512, shm, s>>>(a);
+  gemm_rowblock_kernel<KT, FM, FN, FLAGS><<<grid, 512, shm, s>>>(a);
+}
+
+template <int FLAGS>
+static void launch_rowblock1(const ConvArgs& a, int grid, hipStream_t s) {
+  if (a.K == 320) launch_rowblock2<10, 2, FLAGS>(a, grid, s);
+  else launch_rowblock2<20, 1, FLAGS>(a, grid, s);
 }
 
 // returns false when no instance matches (the caller then uses the tiled kernels)
 static bool launch_rowblock(ConvArgs& a, hipStream_t s) {
   const int flags = (a.ln_mr ? RB_LN : 0) | (a.res ? RB_RES : 0) | (a.rowvec ? RB_RV : 0) |
                     (a.act == LS_ACT_GEGLU ? RB_GEGLU : 0);
-  const int ntm = a.M / 256, nch = a.N / 32;
+  const int bm = a.K == 320 ? 256 : 128;
+  const int ntm = a.M / bm, nch = a.N / 32;
   a.ntm = ntm;
   a.ntn = std::max(1, std::min(nch, (256 + ntm - 1) / ntm));
   const int grid = ntm * a.ntn;
@@ -1635,6 +1649,7 @@ extern "C" int ls_set_tuning(int32_t key, int32_t value) {
     case 4: g_ablate = value; return LS_OK;
     case 5: if (value != 32 && value != 64) return fail(LS_ERR_INVALID, "BK 32 or 64"); g_bk = value; return LS_OK;
     case 6: g_rowblock = value != 0; return LS_OK;
+    case 7: g_rowblock640 = value != 0; return LS_OK;
     default: return fail(LS_ERR_INVALID, "ls_set_tuning: unknown key");
   }
 }

@@ -326,17 +326,20 @@ def test_layernorm_folded_linear(gpu, geglu, pe):
     assert rel_err(y.float().cpu(), y_ref) < 1e-2
 
 
-@pytest.mark.parametrize("M,N,case", [(512, 960, "bias"), (65536, 320, "res"), (4096, 320, "nobias_res_scale"),
-                                      (65536, 1024, "geglu"), (8192, 2560, "ln_geglu"), (65536, 960, "ln_rv")])
-def test_rowblock_gemm(gpu, M, N, case):
-    """The row-block short-K kernel (K = 320, A rows in registers, transposed MFMA,
+@pytest.mark.parametrize("K,M,N,case", [(320, 512, 960, "bias"), (320, 65536, 320, "res"),
+                                        (320, 4096, 320, "nobias_res_scale"), (320, 65536, 1024, "geglu"),
+                                        (320, 8192, 2560, "ln_geglu"), (320, 65536, 960, "ln_rv"),
+                                        (640, 384, 1920, "ln"), (640, 32768, 640, "bias"), (640, 4096, 5120, "ln_geglu"),
+                                        (640, 16384, 1920, "ln_rv")])
+def test_rowblock_gemm(gpu, K, M, N, case):
+    """The row-block short-K kernel (K = 320 / 640, A rows in registers, transposed MFMA,
     register epilogue) for every epilogue flag combination, on N-split grids (small M)
     and the full chunk loop (odd / even chunk counts) -- checked against fp32 on the
     first and last 256 rows, and against the tiled kernel (rowblock off) on all rows.
     Tolerance 1e-2 (bf16 out)."""
     from latentsync_amd import _lib
     lib = _lib.load()
-    K, S, Fr = 320, 1024, 16
+    S, Fr = (1024 if K == 320 else 256), 16
     x = bf(rnd(M, K, seed=90) * (2 if "ln" in case else 1) + (3 if "ln" in case else 0))
     geglu = "geglu" in case
     w = rnd(N, K, seed=91, scale=1 / math.sqrt(K))
