@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LS_ABI_VERSION 3
+#define LS_ABI_VERSION 4
 
 typedef enum {
   LS_OK = 0,
@@ -96,6 +96,11 @@ typedef struct {
   const float* ln_rowstats;  /* NULL or (mean, rstd) per A row (ksize 1 only)  */
   const float* ln_colsum;    /* [N] column sums of Wp (with ln_rowstats)       */
   int32_t rowvec_mod;        /* 0 = none                                       */
+  float* row_stats_out;      /* NULL or fp32 [M][2] (mean, rstd) of each output row (ksize 1,
+                                LayerNorm statistics for the next folded GEMM; the row-block
+                                kernel emits them from its epilogue, other paths run
+                                ls_row_stats on y)                                  */
+  float row_stats_eps;       /* LayerNorm eps of row_stats_out (0 = 1e-5)        */
 } ls_conv_desc;
 
 int ls_conv2d(const ls_conv_desc* d, void* stream);

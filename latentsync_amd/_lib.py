@@ -10,7 +10,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LS_HIP_LIB", os.path.join(HERE, "libls_hip.so"))
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 c_u16p = C.c_void_p
 c_vp = C.c_void_p
@@ -34,6 +34,7 @@ class ConvDesc(C.Structure):
         ("split_k", C.c_int32),
         ("workspace", c_vp), ("workspace_bytes", C.c_size_t),
         ("ln_rowstats", c_vp), ("ln_colsum", c_vp), ("rowvec_mod", C.c_int32),
+        ("row_stats_out", c_vp), ("row_stats_eps", C.c_float),
     ]
 
 

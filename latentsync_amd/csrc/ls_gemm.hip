@@ -30,6 +30,7 @@ struct ConvArgs {
   void* y; int ldy; int y_f32;
   int ktiles, kt_per_split, split; float* partial;
   int ntm, ntn;
+  float* stats_out; float stats_eps;  // row (mean, rstd) of y (row-block epilogue or a trailing row_stats)
   int ablate;  // tuning only (bits): 2 = skip operand DMA, 4 = skip epilogue stores, 8 = skip epilogue,
                // 16 = skip MFMAs (DMA kernel)
 };
@@ -1194,7 +1195,7 @@ __global__ void splitk_reduce_kernel(ConvArgs a) {
 // Host contract (rowblock_ok): ksize 1, no x2 / affine prologue, K = 32*KT = Cin
 // (320 with FM = 2: 256 rows per block; 640 with FM = 1: 128 rows, A still 80 VGPRs),
 // M % BM == 0, N % 64 == 0, no split-K, bf16 output with 4-aligned pitches.
-enum { RB_LN = 1, RB_RES = 2, RB_RV = 4, RB_GEGLU = 8 };
+enum { RB_LN = 1, RB_RES = 2, RB_RV = 4, RB_GEGLU = 8, RB_STATS = 16 };
 
 template <int KT, int FM, int FN, int FLAGS>
 __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
@@ -1204,6 +1205,7 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
   constexpr int WIMG = BN * KTILES * 8;       // uint4 of the W images of a chunk
   constexpr int STAGE = WIMG + 48;            // + bias / colsum / row-vector columns (3 x 64 fp32)
   constexpr bool LN = FLAGS & RB_LN, RES = FLAGS & RB_RES, RV = FLAGS & RB_RV, GG = FLAGS & RB_GEGLU;
+  constexpr bool ST = (FLAGS & RB_STATS) && !GG;  // row statistics of the output (host: one N range per block)
   constexpr int NSTORE = GG ? FM * FN / 2 : FM * FN;
   constexpr int PPT = (WIMG + 511) / 512;     // 16-B DMA pieces per thread per chunk
   static_assert(KT % 2 == 0 && WIMG % 256 == 0, "K must be a multiple of 64");
@@ -1298,8 +1300,14 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
       }
     }
   };
+  double S1[FM], S2[FM];  // running row sums of the output (ST), per lane: its 4-column slices
+#pragma unroll
+  for (int i = 0; i < FM; ++i) { S1[i] = 0.0; S2[i] = 0.0; }
   auto epilogue = [&](int c, const float4 (&bb)[FN], f32x4 (&acc)[FM][FN], const uint2 (&rs)[FM][FN]) {
     const int nb = c * BN + 4 * lg;  // packed column of fragment j: nb + 16 j
+    float cs1[FM], cs2[FM];  // this chunk's partial sums (fp32 over 4*FN values), folded into S in fp64
+#pragma unroll
+    for (int i = 0; i < FM; ++i) { cs1[i] = 0.f; cs2[i] = 0.f; }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
 #pragma unroll
@@ -1326,9 +1334,20 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
           }
 #pragma unroll
           for (int r = 0; r < 4; ++r) o[r] = (acc[i][j][r] + r4[r]) * a.out_scale;
-          *(uint2*)(yrow + nb + 16 * j) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+          const uint2 pk = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+          *(uint2*)(yrow + nb + 16 * j) = pk;
+          if (ST) {  // statistics of the stored (bf16-rounded) values, like ls_row_stats reads them
+            const float b0 = __uint_as_float(pk.x << 16), b1 = __uint_as_float(pk.x & 0xffff0000u);
+            const float b2 = __uint_as_float(pk.y << 16), b3 = __uint_as_float(pk.y & 0xffff0000u);
+            cs1[i] += (b0 + b1) + (b2 + b3);
+            cs2[i] = fmaf(b0, b0, fmaf(b1, b1, fmaf(b2, b2, fmaf(b3, b3, cs2[i]))));
+          }
         }
       }
+    }
+    if (ST) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) { S1[i] += (double)cs1[i]; S2[i] += (double)cs2[i]; }
     }
   };
   auto mfma_chunk = [&](int stage, f32x4 (&acc)[FM][FN]) {
@@ -1392,6 +1411,23 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
   } else {
     load_prm((c1 - 1 - c0) % 3, bb);
     epilogue(c1 - 1, bb, acc0, rsA);
+  }
+  if (ST) {  // the 4 lane groups of a row hold disjoint column slices: combine, then lane group 0 writes
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      double s1 = S1[i], s2 = S2[i];
+#pragma unroll
+      for (int o = 16; o < 64; o <<= 1) {
+        s1 += __shfl_xor(s1, o, 64);
+        s2 += __shfl_xor(s2, o, 64);
+      }
+      if (lg == 0) {
+        const double n = (double)a.N, mean = s1 / n;
+        const double var = fmax(s2 / n - mean * mean, 0.0);
+        *(float2*)(a.stats_out + 2L * (mw + i * 16 + l16)) =
+            make_float2((float)mean, (float)(1.0 / sqrt(var + (double)a.stats_eps)));
+      }
+    }
   }
 }
 
@@ -1470,12 +1506,13 @@ static void launch_rowblock1(const ConvArgs& a, int grid, hipStream_t s) {
 
 // returns false when no instance matches (the caller then uses the tiled kernels)
 static bool launch_rowblock(ConvArgs& a, hipStream_t s) {
-  const int flags = (a.ln_mr ? RB_LN : 0) | (a.res ? RB_RES : 0) | (a.rowvec ? RB_RV : 0) |
-                    (a.act == LS_ACT_GEGLU ? RB_GEGLU : 0);
   const int bm = a.K == 320 ? 256 : 128;
   const int ntm = a.M / bm, nch = a.N / 32;
   a.ntm = ntm;
   a.ntn = std::max(1, std::min(nch, (256 + ntm - 1) / ntm));
+  if (a.stats_out && a.ntn != 1) return false;  // fused statistics need whole rows per block
+  const int flags = (a.ln_mr ? RB_LN : 0) | (a.res ? RB_RES : 0) | (a.rowvec ? RB_RV : 0) |
+                    (a.act == LS_ACT_GEGLU ? RB_GEGLU : 0) | (a.stats_out ? RB_STATS : 0);
   const int grid = ntm * a.ntn;
   switch (flags) {
     case 0: launch_rowblock1<0>(a, grid, s); return true;
@@ -1485,6 +1522,8 @@ static bool launch_rowblock(ConvArgs& a, hipStream_t s) {
     case RB_LN | RB_RES: launch_rowblock1<RB_LN | RB_RES>(a, grid, s); return true;
     case RB_LN | RB_GEGLU: launch_rowblock1<RB_LN | RB_GEGLU>(a, grid, s); return true;
     case RB_GEGLU: launch_rowblock1<RB_GEGLU>(a, grid, s); return true;
+    case RB_STATS: launch_rowblock1<RB_STATS>(a, grid, s); return true;
+    case RB_RES | RB_STATS: launch_rowblock1<RB_RES | RB_STATS>(a, grid, s); return true;
     default: return false;
   }
 }
@@ -1618,6 +1657,10 @@ static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split
   a.rowvec_ld = d->rowvec_ld > 0 ? d->rowvec_ld : d->N;
   a.res = d->res; a.ldr = d->ldr; a.out_scale = d->out_scale == 0.f ? 1.f : d->out_scale; a.act = d->act;
   a.y = d->y; a.ldy = d->ldy; a.y_f32 = d->y_f32;
+  a.stats_out = d->row_stats_out;
+  a.stats_eps = d->row_stats_eps > 0.f ? d->row_stats_eps : 1e-5f;
+  if (a.stats_out && (d->ksize != 1 || d->act == LS_ACT_GEGLU || d->y_f32))
+    return fail(LS_ERR_INVALID, "ls_conv2d: row_stats_out needs ksize 1, bf16 output, no GEGLU");
   a.ablate = g_ablate;
   a.ktiles = d->K / 64;
   t = pick_tile(M, d->N, a.ktiles, d->split_k <= 0 && d->workspace != nullptr,
@@ -1698,6 +1741,14 @@ extern "C" int ls_conv2d(const ls_conv_desc* d, void* stream) {
   }
   hipStream_t s = (hipStream_t)stream;
   if (rowblock_ok(d, a) && launch_rowblock(a, s)) return check_launch("gemm_rowblock_kernel");
+  if (a.stats_out) {  // tiled path: the GEMM, then LayerNorm statistics of y in a second pass
+    float* so = a.stats_out;
+    a.stats_out = nullptr;
+    ls_conv_desc d2 = *d;
+    d2.row_stats_out = nullptr;
+    if ((rc = ls_conv2d(&d2, stream)) != LS_OK) return rc;
+    return ls_row_stats((const uint16_t*)d->y, d->ldy, a.M, d->N, a.stats_eps, so, stream);
+  }
   const bool tapu = (d->ksize == 3) && (a.Cin % 64 == 0);
   const int grid = a.ntm * a.ntn * a.split;
   if (t.bm == 257 && !a.aff_scale && !g_force_regstage && (d->ksize == 1 || tapu)) {  // phased 256x256

@@ -70,10 +70,12 @@ def _ld(t):
 
 
 def conv(x, pw: Packed, *, x2=None, aff=None, stride=1, pad=None, upsample=False, out_hw=None, rowvec=None,
-         res=None, out_scale=1.0, act=ACT_NONE, out=None, out_f32=False, split_k=0, ln_stats=None):
+         res=None, out_scale=1.0, act=ACT_NONE, out=None, out_f32=False, split_k=0, ln_stats=None,
+         stats_out=None):
     """Fused conv/linear.  x (n, H, W, C1) [+ x2 (n, H, W, C2)] -> (n, Ho, Wo, n_out).
     aff = (scale[S][C], shift[S][C], imgs_per_sample, silu); rowvec = (t[S][ld], rows_per_vec, ld[, mod]);
-    ln_stats = (mean, rstd) rows from row_stats(): LayerNorm folded into pw (pw.colsum)."""
+    ln_stats = (mean, rstd) rows from row_stats(): LayerNorm folded into pw (pw.colsum);
+    stats_out = fp32 (rows, 2) receiving row_stats() of the output (eps 1e-5)."""
     lib = _lib.load()
     n, H, W, C1 = x.shape
     C2 = x2.shape[3] if x2 is not None else 0
@@ -114,6 +116,10 @@ def conv(x, pw: Packed, *, x2=None, aff=None, stride=1, pad=None, upsample=False
     assert tuple(out.shape) == (n, Ho, Wo, n_out), (tuple(out.shape), (n, Ho, Wo, n_out))
     d.y, d.ldy, d.y_f32 = _p(out), _ld(out), int(out.dtype == torch.float32)
     d.split_k = split_k
+    if stats_out is not None:
+        assert stats_out.dtype == torch.float32 and stats_out.is_contiguous() and stats_out.numel() == 2 * n * Ho * Wo
+        assert pw.n_out == pw.N and act != ACT_GEGLU, "row statistics over the real output channels only"
+        d.row_stats_out, d.row_stats_eps = _p(stats_out), 1e-5
     d.workspace, d.workspace_bytes = _p(ws.gemm), ws.gemm.numel()
     check(lib.ls_conv2d(C.byref(d), _stream()), "ls_conv2d")
     return out

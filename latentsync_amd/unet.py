@@ -164,26 +164,28 @@ class _Transformer:
         rows = n * HW
         d = C // self.heads
         sc = ops.group_norm(x, self.groups, 1e-6, *self.norm, n)
+        # LayerNorm statistics of every h come out of the GEMM that writes h
+        st = torch.empty((rows, 2), dtype=torch.float32, device=x.device)
         # GN affine materialised (HBM-bound, 2 B/elem each way) so proj_in runs on the DMA GEMM
-        h = ops.conv(ops.group_norm_apply(x, sc[0], sc[1], n, False), self.proj_in).view(rows, C)
+        h = ops.conv(ops.group_norm_apply(x, sc[0], sc[1], n, False), self.proj_in, stats_out=st).view(rows, C)
         # self attention (norm1 folded into the q|k|v GEMM)
-        qkv = ops.linear(h, self.qkv1, ln_stats=ops.row_stats(h))
+        qkv = ops.linear(h, self.qkv1, ln_stats=st)
         o = torch.empty((rows, C), dtype=torch.bfloat16, device=x.device)
         ops.attention(qkv, qkv[:, C:], qkv[:, 2 * C:], o, batch=n, z2=1, heads=self.heads, nq=HW, nk=HW, head_dim=d,
                       qs=(HW * 3 * C, 0, 3 * C, d), ks=(HW * 3 * C, 0, 3 * C, d), vs=(HW * 3 * C, 0, 3 * C, d),
                       os_=(HW * C, 0, C, d))
-        h = ops.linear(o, self.o1, res=h)
+        h = ops.linear(o, self.o1, res=h, stats_out=st)
         # audio cross attention
         if self.has_audio and audio_rows is not None:
-            q = ops.linear(h, self.q2, ln_stats=ops.row_stats(h))
+            q = ops.linear(h, self.q2, ln_stats=st)
             kv = ops.linear(audio_rows, self.kv2)
             L = n_audio_tok
             ops.attention(q, kv, kv[:, C:], o, batch=n, z2=1, heads=self.heads, nq=HW, nk=L, head_dim=d,
                           qs=(HW * C, 0, C, d), ks=(L * 2 * C, 0, 2 * C, d), vs=(L * 2 * C, 0, 2 * C, d),
                           os_=(HW * C, 0, C, d))
-            h = ops.linear(o, self.o2, res=h)
+            h = ops.linear(o, self.o2, res=h, stats_out=st)
         # GEGLU feed-forward (norm3 folded)
-        g = ops.linear(h, self.ff1, act=ops.ACT_GEGLU, ln_stats=ops.row_stats(h))
+        g = ops.linear(h, self.ff1, act=ops.ACT_GEGLU, ln_stats=st)
         h = ops.linear(g, self.ff2, res=h)
         return ops.conv(h.view(n, H, W, C), self.proj_out, res=x)
 
@@ -224,19 +226,20 @@ class _Motion:
         rows = n * S
         d = C // self.heads
         sc = ops.group_norm(x, self.groups, 1e-6, *self.norm, n)
+        lns = torch.empty((rows, 2), dtype=torch.float32, device=x.device)  # LN stats of h, from its GEMM
         # GN affine materialised (HBM-bound, 2 B/elem each way) so proj_in runs on the DMA GEMM
-        h = ops.conv(ops.group_norm_apply(x, sc[0], sc[1], n, False), self.proj_in).view(rows, C)
+        h = ops.conv(ops.group_norm_apply(x, sc[0], sc[1], n, False), self.proj_in, stats_out=lns).view(rows, C)
         o = torch.empty((rows, C), dtype=torch.bfloat16, device=x.device)
         for a in self.attn:
             pk = a["qkv"]  # LN (+ positional encoding, as the W pe row table) folded in
             rv = (pk.pe_rows, S, pk.pe_rows.shape[1], F) if pk.pe_rows is not None else None
-            qkv = ops.linear(h, pk, ln_stats=ops.row_stats(h), rowvec=rv)
+            qkv = ops.linear(h, pk, ln_stats=lns, rowvec=rv)
             # "(b f) s c -> (b s) f c": batch (b, s), sequence f
             st = (F * S * 3 * C, 3 * C, S * 3 * C, d)
             ops.attention(qkv, qkv[:, C:], qkv[:, 2 * C:], o, batch=B * S, z2=S, heads=self.heads, nq=F, nk=F,
                           head_dim=d, qs=st, ks=st, vs=st, os_=(F * S * C, C, S * C, d))
-            h = ops.linear(o, a["o"], res=h)
-        g = ops.linear(h, self.ff1, act=ops.ACT_GEGLU, ln_stats=ops.row_stats(h))
+            h = ops.linear(o, a["o"], res=h, stats_out=lns)
+        g = ops.linear(h, self.ff1, act=ops.ACT_GEGLU, ln_stats=lns)
         h = ops.linear(g, self.ff2, res=h)
         return ops.conv(h.view(n, H, W, C), self.proj_out, res=x)
 

@@ -23,6 +23,7 @@ from latentsync_amd.vae import AutoencoderKL  # noqa: E402
 def main():
     nw = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     R = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+    phase = sys.argv[3] if len(sys.argv) > 3 else "step"  # step | encode | decode
     dev = torch.device("cuda", 0)
     unet = UNet3DConditionModel(**STAGE2_MODEL).init_weights(41).to(dev).eval()
     vae = AutoencoderKL().init_weights(51).to(dev)
@@ -68,7 +69,7 @@ def main():
 
     for n in names:
         setattr(ops, n, wrap(n))
-    eng._step()
+    {"step": eng._step, "encode": eng._encode, "decode": eng._decode}[phase]()
     torch.cuda.synchronize()
     for n in names:
         setattr(ops, n, orig[n])
@@ -80,7 +81,7 @@ def main():
         agg[key][1] += t
         agg[key][2] += fl
         tot += t
-    print(f"step: {len(recs)} calls, {tot:.3f} ms summed (windows={nw}, R={R})")
+    print(f"{phase}: {len(recs)} calls, {tot:.3f} ms summed (windows={nw}, R={R})")
     fam = collections.defaultdict(float)
     for (n, _), (c, t, fl) in agg.items():
         fam[n] += t

@@ -380,3 +380,20 @@ def test_rowblock_gemm(gpu, K, M, N, case):
         lib.ls_set_tuning(6, 1)
     assert rel_err(y.float().cpu()[rows], ref) < 1e-2
     assert rel_err(y.float(), y_tiled.float()) < 1e-2
+
+
+@pytest.mark.parametrize("K,M,N,res", [(320, 65536, 320, True), (320, 8192, 320, False), (640, 4096, 640, False),
+                                       (640, 4096, 640, True), (1280, 2048, 1280, True), (320, 512, 320, True)])
+def test_linear_row_stats_out(gpu, K, M, N, res):
+    """LayerNorm row statistics of a linear's output emitted with it (row-block epilogue
+    when one block owns whole rows, else a trailing ls_row_stats): equal to row_stats()
+    of the stored output.  Tolerance 1e-4 (mean) / 1e-3 (rstd)."""
+    x = bf(rnd(M, K, seed=97)).to(torch.bfloat16).to(DEV)
+    w = rnd(N, K, seed=98, scale=1 / math.sqrt(K))
+    b = rnd(N, seed=99, scale=0.5) + 2.0  # rows with |mean| > std
+    kw = {"res": bf(rnd(M, N, seed=100)).to(torch.bfloat16).to(DEV)} if res else {}
+    st = torch.empty((M, 2), dtype=torch.float32, device=DEV)
+    y = ops.linear(x, packed(w, b, 1), stats_out=st, **kw)
+    ref = ops.row_stats(y)
+    assert (st[:, 0] - ref[:, 0]).abs().max().item() < 1e-4 * max(1.0, ref[:, 0].abs().max().item())
+    assert ((st[:, 1] - ref[:, 1]).abs() / ref[:, 1]).max().item() < 1e-3
