@@ -1,7 +1,7 @@
 """Benchmark: lip-synced frames/sec at 256x256, 16-frame window, 20 DDIM steps
 (BASELINE.json "metric", configs[1]; configs[3] when launched on N GPUs).
 
-One "step" = one batch of `--windows-per-batch` (default 8) independent
+One "step" = one batch of `--windows-per-batch` (default 16) independent
 16-frame windows of a clip through the whole hot path on one GPU: pixel prep ->
 VAE encode x2 -> 20 x (UNet3D fwd + CFG + DDIM) -> VAE decode -> paste-back,
 inputs resident in HBM.  Every window is computed exactly as alone (per-window
@@ -41,9 +41,11 @@ WORK_TF = {256: (4.0505, 0.2727, 0.6222), 512: (17.626, 1.1167, 2.5145)}
 PEAK_BF16_TF = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 # BASELINE.json configs this bench can run on one GPU (configs[0] is the CPU-only
 # plumbing case, configs[3] is configs[1] sharded over 8 ranks)
+# windows: independent 16-frame windows of a clip batched per UNet call (measured on MI355X:
+# 8 -> 110.2, 16 -> 113.3 frames/s at configs[1], gpurun_out/p23.log)
 PRESETS = {
-    1: dict(resolution=256, guidance=1.0, steps=20, windows=8),
-    2: dict(resolution=256, guidance=2.0, steps=50, windows=4),
+    1: dict(resolution=256, guidance=1.0, steps=20, windows=16),
+    2: dict(resolution=256, guidance=2.0, steps=50, windows=8),
     4: dict(resolution=512, guidance=1.0, steps=20, windows=2),
 }
 
