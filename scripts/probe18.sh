@@ -1,3 +1,3 @@
 set -o pipefail
 mkdir -p gpurun_out
-GEMM_EPI=res GEMM_ONLY=conv0,conv1,conv2,"conv up0" timeout -k 10 300 python -u scripts/gemm_bench.py dma@8 dma+t10@8 dma+bk32@8 > gpurun_out/p18_gemm.log 2>&1
+GEMM_EPI=res GEMM_ONLY=conv0,conv1,conv2,"conv up0" timeout -k 10 300 python -u scripts/gemm_bench.py dma@8 > gpurun_out/p18_gemm.log 2>&1
