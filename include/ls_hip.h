@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LS_ABI_VERSION 4
+#define LS_ABI_VERSION 5
 
 typedef enum {
   LS_OK = 0,
@@ -259,6 +259,38 @@ int ls_log_mel(const float* audio, int64_t n_samples, const float* filters, int3
  * out [n_chunks][(left + right + 1) * 2 * layers][C], bf16 or fp32 (out_f32). */
 int ls_audio_chunks(const uint16_t* feat, int64_t ld_row, int32_t T, int32_t layers, int32_t C, int32_t n_chunks,
                     double fps, int32_t left, int32_t right, void* out, int32_t out_f32, void* stream);
+
+/* ---- paste-back warp (restore_video), SURVEY.md §8(f) row 1 ---------------------- */
+
+/* torchvision resize(face, (out_h, out_w), antialias=True) (aten _upsample_bilinear2d_aa)
+ * followed by (x / 2 + 0.5).clamp(0, 1) * 255 -> uint8, as LipsyncPipeline.restore_video
+ * does per face (lipsync_pipeline.py:348-354).  faces fp32 NCHW [N][3][in_h][in_w];
+ * out uint8 HWC [N][out_h][out_w][3]. */
+int ls_face_resize_u8(const float* faces, int32_t N, int32_t in_h, int32_t in_w, int32_t out_h, int32_t out_w,
+                      uint8_t* out, void* stream);
+
+/* Constant tables of the warp (OpenCV initInterTab2D Lanczos4 fixed-point coefficients,
+ * getGaussianKernel(2 w + 1, 0) for w = 0..w_edge_max), computed on the host and copied
+ * into the caller's device buffer `tables` of ls_restore_tables_bytes(w_edge_max) bytes.
+ * Synchronises `stream` (initialisation only; not capturable). */
+size_t ls_restore_tables_bytes(int32_t w_edge_max);
+int ls_restore_init_tables(void* tables, int32_t w_edge_max, void* stream);
+
+/* AlignRestore.restore_img (affine_transform.py:85-115, upscale_factor 1) for N frames,
+ * in place: frames uint8 [N][H][W][3]; faces uint8 [N][fh][fw][3] (the resized faces);
+ * warp fp64 [N][6] = the frame->face matrix cv2.warpAffine iterates with (the inverse of
+ * invertAffineTransform(affine_matrix), in warpAffine's own operation order);
+ * roi int32 [N][4] (x0, y0, x1, y1), 16-byte aligned: the frame box outside which the
+ * soft mask is 0 (width <= roi_w, height <= roi_h); w_edge_max bounds
+ * int(sqrt(mask area)) // 20 and must not exceed the tables' bound.
+ * Per pixel of the ROI: warpAffine(ones) bilinear -> 2x2 erode -> area (fp64) ->
+ * (2 w_edge)^2 erode -> (2 w_edge + 1)^2 Gaussian (BORDER_REFLECT_101) -> soft;
+ * frame = trunc(soft * mask_e * lanczos4(face) + (1 - soft) * frame).
+ * Workspace: ls_restore_workspace_bytes(N, roi_h, roi_w). */
+size_t ls_restore_workspace_bytes(int32_t N, int32_t roi_h, int32_t roi_w);
+int ls_restore_frames(uint8_t* frames, int32_t N, int32_t H, int32_t W, const uint8_t* faces, int32_t fh, int32_t fw,
+                      const double* warp, const int32_t* roi, int32_t roi_h, int32_t roi_w, int32_t w_edge_max,
+                      const void* tables, void* workspace, size_t workspace_bytes, void* stream);
 
 int ls_abi_version(void);
 const char* ls_last_error(void);

@@ -10,7 +10,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LS_HIP_LIB", os.path.join(HERE, "libls_hip.so"))
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 c_u16p = C.c_void_p
 c_vp = C.c_void_p
@@ -78,6 +78,12 @@ _SIGS = {
     "ls_log_mel": (C.c_int, [c_vp, C.c_int64, c_vp, C.c_int32, C.c_int64, c_vp, c_vp, C.c_size_t, c_vp]),
     "ls_audio_chunks": (C.c_int, [c_vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_double,
                                   C.c_int32, C.c_int32, c_vp, C.c_int32, c_vp]),
+    "ls_face_resize_u8": (C.c_int, [c_vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, c_vp, c_vp]),
+    "ls_restore_tables_bytes": (C.c_size_t, [C.c_int32]),
+    "ls_restore_init_tables": (C.c_int, [c_vp, C.c_int32, c_vp]),
+    "ls_restore_workspace_bytes": (C.c_size_t, [C.c_int32, C.c_int32, C.c_int32]),
+    "ls_restore_frames": (C.c_int, [c_vp, C.c_int32, C.c_int32, C.c_int32, c_vp, C.c_int32, C.c_int32, c_vp, c_vp,
+                                    C.c_int32, C.c_int32, C.c_int32, c_vp, c_vp, C.c_size_t, c_vp]),
     "ls_add_rows": (C.c_int, [c_vp, C.c_int64, C.c_int32, C.c_int32, c_vp, C.c_int32, c_vp, C.c_int32, c_vp]),
 }
 
@@ -92,6 +98,12 @@ def load(path: str = None):
     if _lib is not None:
         return _lib
     path = path or os.environ.get("LS_HIP_LIB") or LIB_PATH  # LS_HIP_LIB: A/B builds in tools
+    # torch first: its wheel bundles a HIP runtime with the same soname
+    # (libamdhip64.so.7) as /opt/rocm's.  Loaded in this order the library binds to
+    # torch's runtime, so torch's streams and allocations are valid for the kernels;
+    # loaded first, it would pull in the second runtime and launches fail with
+    # "no ROCm-capable device is detected" (gpurun_out/r01f_smoke.log).
+    import torch  # noqa: F401
     if not os.path.exists(path):
         raise RuntimeError(f"libls_hip.so not found at {path}: run `python -m latentsync_amd.build` "
                            "(the HIP library is required; there is no fallback path)")

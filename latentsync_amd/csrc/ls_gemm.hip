@@ -640,31 +640,11 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_gemm_dma_kernel(ConvArgs a)
     brow[p] = n0 + row;
     bch[p] = swz_bk<BK>(row, q % CPR) - row * CPR;
   }
-  // A-operand source addresses advance by BK elements per K-tile inside a 3x3 tap (TAPU) or
-  // a concat source (1x1): recomputed (a_src: tap / halo / bounds / concat select) only where
-  // a tap or source starts -- per K-tile the address VALU shrinks to one 64-bit add per piece.
-  // Out-of-range pieces sit on the zero page with step 0.
-  const u16* aptr[AI];
-  int astep[AI];
-  bool a_first = true;
   auto issue = [&](int kt, int stage) {
     uint4* base = lds + stage * STAGE;
-    const int kk = kt * BK;
-    bool fresh = a_first;
-    if (KS == 3 && TAPU) { const int r = kk % a.Cin; fresh |= (r == 0) | (r == a.C1); }
-    else if (KS == 1) fresh |= (kk == a.C1) | (kk >= a.Cin);
-    else fresh = true;
-    a_first = false;
 #pragma unroll
-    for (int p = 0; p < AI; ++p) {
-      if (fresh) {
-        aptr[p] = (const u16*)a_src<KS, TAPU, BK>(a, kt, ach[p], arow[p], geo[p]);
-        astep[p] = aptr[p] == (const u16*)ls_zero_page ? 0 : BK;
-      } else {
-        aptr[p] += astep[p];
-      }
-      glds16(aptr[p], base + (wid * AI + p) * 64);
-    }
+    for (int p = 0; p < AI; ++p)
+      glds16(a_src<KS, TAPU, BK>(a, kt, ach[p], arow[p], geo[p]), base + (wid * AI + p) * 64);
 #pragma unroll
     for (int p = 0; p < BI; ++p) {
       const void* src = brow[p] < a.N ? (const void*)(a.w + (long)brow[p] * a.K + kt * BK + bch[p] * 8)
@@ -797,31 +777,11 @@ __global__ void __launch_bounds__(512) conv_gemm_big_kernel(ConvArgs a) {
     brow[p] = n0 + row;
     bch[p] = swz_bk<BK>(row, q % CPR) - row * CPR;
   }
-  // A-operand source addresses advance by BK elements per K-tile inside a 3x3 tap (TAPU) or
-  // a concat source (1x1): recomputed (a_src: tap / halo / bounds / concat select) only where
-  // a tap or source starts -- per K-tile the address VALU shrinks to one 64-bit add per piece.
-  // Out-of-range pieces sit on the zero page with step 0.
-  const u16* aptr[AI];
-  int astep[AI];
-  bool a_first = true;
   auto issue = [&](int kt, int stage) {
     uint4* base = lds + stage * STAGE;
-    const int kk = kt * BK;
-    bool fresh = a_first;
-    if (KS == 3 && TAPU) { const int r = kk % a.Cin; fresh |= (r == 0) | (r == a.C1); }
-    else if (KS == 1) fresh |= (kk == a.C1) | (kk >= a.Cin);
-    else fresh = true;
-    a_first = false;
 #pragma unroll
-    for (int p = 0; p < AI; ++p) {
-      if (fresh) {
-        aptr[p] = (const u16*)a_src<KS, TAPU, BK>(a, kt, ach[p], arow[p], geo[p]);
-        astep[p] = aptr[p] == (const u16*)ls_zero_page ? 0 : BK;
-      } else {
-        aptr[p] += astep[p];
-      }
-      glds16(aptr[p], base + (wid * AI + p) * 64);
-    }
+    for (int p = 0; p < AI; ++p)
+      glds16(a_src<KS, TAPU, BK>(a, kt, ach[p], arow[p], geo[p]), base + (wid * AI + p) * 64);
 #pragma unroll
     for (int p = 0; p < BI; ++p) {
       const void* src = brow[p] < a.N ? (const void*)(a.w + (long)brow[p] * a.K + kt * BK + bch[p] * 8)
@@ -1113,31 +1073,11 @@ __global__ void __launch_bounds__(512) conv_gemm_big4_kernel(ConvArgs a) {
     brow[p] = n0 + row;
     bch[p] = swz_bk<BK>(row, q % CPR) - row * CPR;
   }
-  // A-operand source addresses advance by BK elements per K-tile inside a 3x3 tap (TAPU) or
-  // a concat source (1x1): recomputed (a_src: tap / halo / bounds / concat select) only where
-  // a tap or source starts -- per K-tile the address VALU shrinks to one 64-bit add per piece.
-  // Out-of-range pieces sit on the zero page with step 0.
-  const u16* aptr[AI];
-  int astep[AI];
-  bool a_first = true;
   auto issue = [&](int kt, int stage) {
     uint4* base = lds + stage * STAGE;
-    const int kk = kt * BK;
-    bool fresh = a_first;
-    if (KS == 3 && TAPU) { const int r = kk % a.Cin; fresh |= (r == 0) | (r == a.C1); }
-    else if (KS == 1) fresh |= (kk == a.C1) | (kk >= a.Cin);
-    else fresh = true;
-    a_first = false;
 #pragma unroll
-    for (int p = 0; p < AI; ++p) {
-      if (fresh) {
-        aptr[p] = (const u16*)a_src<KS, TAPU, BK>(a, kt, ach[p], arow[p], geo[p]);
-        astep[p] = aptr[p] == (const u16*)ls_zero_page ? 0 : BK;
-      } else {
-        aptr[p] += astep[p];
-      }
-      glds16(aptr[p], base + (wid * AI + p) * 64);
-    }
+    for (int p = 0; p < AI; ++p)
+      glds16(a_src<KS, TAPU, BK>(a, kt, ach[p], arow[p], geo[p]), base + (wid * AI + p) * 64);
 #pragma unroll
     for (int p = 0; p < BI; ++p) {
       const void* src = brow[p] < a.N ? (const void*)(a.w + (long)brow[p] * a.K + kt * BK + bch[p] * 8)
