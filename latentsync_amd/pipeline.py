@@ -48,6 +48,39 @@ def load_fixed_mask(resolution=256, mask_image_path=None):
     return t
 
 
+def load_data_pth(data_path):
+    """The precomputed ingest file (affine_transform_video.py:30-35 writes it;
+    lipsync_pipeline.py:398-402 reads it): {faces uint8 (N,3,R,R), boxes, affine_matrices}.
+    The matrices are cv2's float64 numpy arrays, so the weights-only unpickler is
+    widened by exactly numpy's array reconstruction (ndarray, dtype, _reconstruct and
+    the concrete dtype classes) -- still nothing from the file is executed."""
+    allow = [np.ndarray, np.dtype, np._core.multiarray._reconstruct]
+    allow += [type(np.dtype(t)) for t in ("f8", "f4", "i8", "i4", "u1")]
+    with torch.serialization.safe_globals(allow):
+        data = torch.load(data_path, map_location="cpu", weights_only=True)
+    data["affine_matrices"] = [np.asarray(m, np.float64).reshape(2, 3) for m in data["affine_matrices"]]
+    return data
+
+
+def read_video_frames(video_path):
+    """Original video frames for restore_video: read_video (util.py:46-100) decodes
+    with ffmpeg/cv2, which this build does not carry, so the frames come already
+    decoded -- a uint8 (N,H,W,3) .npy, or an .npz holding ``frames``.  Any other
+    path returns None (no warp-back; the aligned faces are written)."""
+    if not video_path or not os.path.exists(video_path):
+        return None
+    if video_path.endswith(".npy"):
+        fr = np.load(video_path, allow_pickle=False)
+    elif video_path.endswith(".npz"):
+        with np.load(video_path, allow_pickle=False) as z:
+            fr = z["frames"]
+    else:
+        return None
+    if fr.dtype != np.uint8 or fr.ndim != 4 or fr.shape[-1] != 3:
+        raise ValueError(f"{video_path}: expected uint8 frames (N,H,W,3), got {fr.dtype} {fr.shape}")
+    return fr
+
+
 class WindowEngine:
     """Device-resident executor of one 16-frame window; see module docstring."""
 
@@ -277,17 +310,31 @@ class LipsyncPipeline:
         loc8 = torch.stack(outs_u8) if outs_u8 else torch.empty((0, F_, R, R, 3), dtype=torch.uint8, device=dev)
         return (shard.gather_windows(loc, n_inf).flatten(0, 1), shard.gather_windows(loc8, n_inf).flatten(0, 1))
 
+    def restore_video(self, faces, video_frames, boxes, affine_matrices):
+        """:343-358 on the device (latentsync_amd/restore.py): every face of the clip
+        resized in one launch, then warped and blended into its frame.  Returns the
+        restored frames (N,H,W,3) uint8 on the device (the reference returns numpy)."""
+        from . import restore
+        if getattr(self, "_restorer", None) is None:
+            self._restorer = restore.AlignRestore(self.device)
+        return restore.restore_video(faces, video_frames, boxes, affine_matrices, self._restorer)
+
     @torch.no_grad()
     def __call__(self, video_path, audio_path, video_out_path, video_mask_path=None, num_frames=16, video_fps=25,
                  audio_sample_rate=16000, height=None, width=None, num_inference_steps=20, guidance_scale=1.5,
                  weight_dtype=torch.float16, eta=0.0, mask="fix_mask", mask_image_path="latentsync/utils/mask.png",
                  generator=None, callback=None, callback_steps=1, data_path=None, start_from_backwards=False,
                  force_video_length=False, use_darken=False, brightness_factor=1.0, **kwargs):
-        """:360-604.  Face alignment, restore_video (cv2 warp-back) and ffmpeg
-        muxing are CPU I/O outside this build's scope; the
-        precomputed ``data_path`` (.pth {faces, boxes, affine_matrices}) is the
-        supported face source and the output is written as an .npz of the
-        lip-synced face frames (uint8) plus the aligned audio."""
+        """:360-604.  Face detection / alignment and the ffmpeg decode, encode and
+        mux are outside this build's scope: the precomputed
+        ``data_path`` (.pth {faces, boxes, affine_matrices}, :398-402) is the face
+        source and ``video_path`` holds the original frames already decoded, as a
+        uint8 (N,H,W,3) ``.npy`` or an ``.npz`` with a ``frames`` array
+        (read_video's output, util.py:46-100).  The synced faces are pasted back into
+        those frames on the GPU (restore_video, :577) and the result is written as an
+        .npz of the restored frames (uint8) plus the aligned audio.  With
+        ``faces_only=True`` (or a video_path that is not an array file) the
+        lip-synced aligned faces are written instead and no warp-back happens."""
         from . import repeat as rep
         if eta != 0.0:
             raise NotImplementedError("eta > 0")
@@ -295,7 +342,7 @@ class LipsyncPipeline:
             raise NotImplementedError("only mask='fix_mask' is on the inference path")
         if not data_path:
             raise NotImplementedError("face detection / alignment is out of scope: pass data_path (.pth)")
-        data = torch.load(data_path, map_location="cpu", weights_only=True)
+        data = load_data_pth(data_path)
         faces = data["faces"]
         R = height or faces.shape[-1]
         self.check_inputs(R, width or R, callback_steps)
@@ -325,9 +372,13 @@ class LipsyncPipeline:
         chunks = torch.stack([c.to(self.device) for c in chunks])
         out, out_u8 = self.run_windows(faces, chunks, keep, num_frames, num_inference_steps, guidance_scale,
                                        generator, callback=callback, callback_steps=callback_steps)
-        n_out = out_u8.shape[0]
+        frames_out = out_u8
+        video_frames = None if kwargs.get("faces_only") else read_video_frames(video_path)
+        if video_frames is not None:
+            frames_out = self.restore_video(out, video_frames, data["boxes"], data["affine_matrices"])
+        n_out = frames_out.shape[0]
         audio_keep = int(n_out / video_fps * audio_sample_rate)
         np.savez(video_out_path if video_out_path.endswith(".npz") else video_out_path + ".npz",
-                 frames=out_u8.cpu().numpy(), audio=np.asarray(audio_samples[:audio_keep]),
+                 frames=frames_out.cpu().numpy(), audio=np.asarray(audio_samples[:audio_keep]),
                  fps=video_fps, sample_rate=audio_sample_rate, padding_duration=padding_duration)
         return None

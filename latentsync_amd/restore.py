@@ -147,6 +147,10 @@ def restore_video(faces, video_frames, boxes, affine_matrices, restorer=None):
     Returns the restored frames (N,H,W,3) uint8 on the device."""
     restorer = restorer or AlignRestore(faces.device)
     N = faces.shape[0]
+    if len(boxes) < N or len(affine_matrices) < N or len(video_frames) < N:
+        # the reference indexes boxes[index] / affine_matrices[index] per face (:347, :356)
+        raise IndexError(f"restore_video: {N} faces but {len(boxes)} boxes, {len(affine_matrices)} matrices, "
+                         f"{len(video_frames)} frames")
     frames = torch.as_tensor(np.asarray(video_frames[:N])) if not torch.is_tensor(video_frames) else video_frames[:N]
     frames = frames.to(faces.device, torch.uint8).contiguous().clone()
     sizes = [(int(b[3] - b[1]), int(b[2] - b[0])) for b in boxes[:N]]

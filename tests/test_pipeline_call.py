@@ -1,0 +1,130 @@
+"""LipsyncPipeline.__call__ end to end (lipsync_pipeline.py:361-604) on the data.pth
+ingest path: faces / boxes / affine matrices from a .pth (:398-402), original frames
+already decoded (.npy / .npz), Whisper features, the window loop and the warp-back
+(restore_video, :577) on the device, audio trimmed to the output length (:580-581).
+
+The window loop itself is pinned by tests/test_gpu_pipeline.py and the warp-back by
+tests/test_restore.py; here the GPU restore inside __call__ is checked against the CPU
+restatement (oracle/restore_cpu.py) on exactly the faces the loop produced."""
+import math
+import wave
+
+import numpy as np
+import pytest
+import torch
+
+from latentsync_amd.pipeline import LipsyncPipeline, load_data_pth, read_video_frames
+
+SCHED = dict(beta_end=0.012, beta_schedule="scaled_linear", beta_start=0.00085, clip_sample=False,
+             num_train_timesteps=1000, set_alpha_to_one=False, steps_offset=1)
+
+
+def _align(cx, cy, s, theta, fh, fw):
+    c, sn = math.cos(theta) * s, math.sin(theta) * s
+    R = np.array([[c, -sn], [sn, c]])
+    t = np.array([fw / 2.0, fh / 2.0]) - R @ np.array([cx, cy])
+    return np.concatenate([R, t[:, None]], axis=1)
+
+
+def _write_wav(path, seconds, sr=16000, seed=1):
+    a = np.random.default_rng(seed).normal(0, 0.1, int(seconds * sr)).clip(-1, 0.999)
+    with wave.open(str(path), "wb") as f:
+        f.setnchannels(1)
+        f.setsampwidth(2)
+        f.setframerate(sr)
+        f.writeframes((a * 32768).astype("<i2").tobytes())
+
+
+def test_read_video_frames(tmp_path):
+    fr = np.random.default_rng(0).integers(0, 256, (3, 20, 30, 3), dtype=np.uint8)
+    np.save(tmp_path / "v.npy", fr)
+    np.savez(tmp_path / "v.npz", frames=fr)
+    assert np.array_equal(read_video_frames(str(tmp_path / "v.npy")), fr)
+    assert np.array_equal(read_video_frames(str(tmp_path / "v.npz")), fr)
+    assert read_video_frames(str(tmp_path / "missing.mp4")) is None
+    np.save(tmp_path / "bad.npy", fr.astype(np.float32))
+    with pytest.raises(ValueError):
+        read_video_frames(str(tmp_path / "bad.npy"))
+
+
+def test_load_data_pth_numpy_matrices(tmp_path):
+    """cv2 writes the affine matrices as float64 numpy arrays; the weights-only loader
+    takes them (and plain tensors / lists) and refuses anything else."""
+    mats = [np.arange(6, dtype=np.float64).reshape(2, 3) + i for i in range(3)]
+    faces = torch.zeros((3, 3, 8, 8), dtype=torch.uint8)
+    torch.save({"faces": faces, "boxes": [[0, 0, 48, 56]] * 3, "affine_matrices": mats}, tmp_path / "d.pth")
+    d = load_data_pth(str(tmp_path / "d.pth"))
+    assert torch.equal(d["faces"], faces) and d["boxes"][0] == [0, 0, 48, 56]
+    assert all(np.array_equal(a, b) and a.dtype == np.float64 for a, b in zip(d["affine_matrices"], mats))
+    torch.save({"faces": faces, "boxes": [[0, 0, 8, 8]] * 3,
+                "affine_matrices": [torch.from_numpy(m) for m in mats]}, tmp_path / "t.pth")
+    assert np.array_equal(load_data_pth(str(tmp_path / "t.pth"))["affine_matrices"][2], mats[2])
+
+    class Evil:
+        def __reduce__(self):
+            return (print, ("executed",))
+
+    torch.save({"faces": faces, "boxes": [], "affine_matrices": [Evil()]}, tmp_path / "e.pth")
+    with pytest.raises(Exception):
+        load_data_pth(str(tmp_path / "e.pth"))
+
+
+@pytest.mark.gpu
+def test_call_data_pth_with_restore(tmp_path, monkeypatch):
+    from latentsync_amd.audio import Audio2Feature
+    from latentsync_amd.config import TINY_MODEL
+    from latentsync_amd.scheduler import DDIMScheduler
+    from latentsync_amd.unet import UNet3DConditionModel
+    from latentsync_amd.vae import AutoencoderKL
+    from oracle import restore_cpu as O
+
+    Rr, Fr, H, W = 64, 8, 120, 160
+    fh, fw = 56, 48
+    unet = UNet3DConditionModel(**TINY_MODEL).init_weights(3).to("cuda").eval()
+    vae = AutoencoderKL(block_out_channels=(32, 64, 64, 64)).init_weights(4).to("cuda")
+    pipe = LipsyncPipeline(vae, Audio2Feature.random(2, device="cuda"), unet, DDIMScheduler(**SCHED))
+    _write_wav(tmp_path / "audio.wav", 0.88)
+    # more video frames than padded audio chunks: the output has one frame per chunk
+    # (restore_video slices video_frames[:len(faces)], :344) and every output frame has
+    # its box / matrix (the reference indexes them per output frame)
+    N = 48
+
+    g = torch.Generator().manual_seed(5)
+    faces = (torch.rand((N, 3, Rr, Rr), generator=g) * 255).to(torch.uint8)
+    rng = np.random.default_rng(6)
+    mats = [_align(80 + rng.uniform(-5, 5), 60 + rng.uniform(-5, 5), rng.uniform(0.8, 1.2),
+                   rng.uniform(-0.15, 0.15), fh, fw) for _ in range(N)]
+    boxes = [[0, 0, fw, fh]] * N
+    torch.save({"faces": faces, "boxes": boxes, "affine_matrices": mats}, tmp_path / "data.pth")
+    frames = rng.integers(0, 256, (N, H, W, 3), dtype=np.uint8)
+    np.save(tmp_path / "video.npy", frames)
+
+    seen = {}
+    real = pipe.restore_video
+
+    def spy(f, v, b, m):
+        seen["faces"] = f.detach().float().cpu()
+        return real(f, v, b, m)
+
+    monkeypatch.setattr(pipe, "restore_video", spy)
+    out_path = str(tmp_path / "out.npz")
+    pipe(video_path=str(tmp_path / "video.npy"), audio_path=str(tmp_path / "audio.wav"), video_out_path=out_path,
+         num_frames=Fr, num_inference_steps=2, guidance_scale=1.0, data_path=str(tmp_path / "data.pth"),
+         mask_image_path=None, generator=torch.Generator(device="cuda").manual_seed(1247))
+    res = np.load(out_path)
+    out = res["frames"]
+    n = out.shape[0]
+    assert 0 < n < N and n % Fr == 0 and out.shape[1:] == (H, W, 3) and out.dtype == np.uint8
+    assert seen["faces"].shape == (n, 3, Rr, Rr)
+    assert 0 < res["audio"].shape[0] <= int(n / 25 * 16000)  # [:remain_length] of the padded audio (:580-581)
+    ref = O.restore_video(seen["faces"], frames, boxes, mats)
+    d = np.abs(out.astype(np.int32) - ref.astype(np.int32))
+    # bit-exact up to the pinned resize's rare 1-LSB rounding (tests/test_restore.py)
+    assert d.max() <= 1 and (d > 0).mean() < 1e-3, (d.max(), (d > 0).mean())
+    assert (out != frames[:n]).any()
+
+    # faces_only: the aligned lip-synced faces, no warp-back
+    pipe(video_path=str(tmp_path / "video.npy"), audio_path=str(tmp_path / "audio.wav"), video_out_path=out_path,
+         num_frames=Fr, num_inference_steps=2, guidance_scale=1.0, data_path=str(tmp_path / "data.pth"),
+         mask_image_path=None, faces_only=True)
+    assert np.load(out_path)["frames"].shape == (n, Rr, Rr, 3)
