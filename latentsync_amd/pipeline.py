@@ -372,6 +372,8 @@ class LipsyncPipeline:
         chunks = torch.stack([c.to(self.device) for c in chunks])
         out, out_u8 = self.run_windows(faces, chunks, keep, num_frames, num_inference_steps, guidance_scale,
                                        generator, callback=callback, callback_steps=callback_steps)
+        if shard.world_and_rank()[1] != 0:
+            return None  # every rank holds the gathered clip; rank 0 restores and writes it
         frames_out = out_u8
         video_frames = None if kwargs.get("faces_only") else read_video_frames(video_path)
         if video_frames is not None:
