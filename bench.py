@@ -7,19 +7,31 @@ VAE encode x2 -> 20 x (UNet3D fwd + CFG + DDIM) -> VAE decode -> paste-back,
 inputs resident in HBM.  Every window is computed exactly as alone (per-window
 GroupNorm statistics / temporal attention; tests/test_gpu_pipeline.py); the
 batch only makes each kernel launch larger.  The JSON also reports the latency
-of a single window run alone (`single_window`).  With N ranks (one process per GPU,
-torch.distributed over RCCL) every rank runs its own windows (weak scaling) and
-the decoded uint8 frames of all ranks are all-gathered once at the end of the
-timed loop (the only collective).  Prints ONE JSON line on rank 0.
+of a single window run alone (`single_window`).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--guidance 1.0]
+Multi-GPU (configs[3]): one process per GPU.  `--gpus N` run
+directly spawns N fresh worker processes of this script (RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_* in their environment) BEFORE anything touches the GPU and
+exits with the first failing worker's status; under torchrun the process is
+already a worker.  Every rank runs its own windows (weak scaling; rank r owns
+windows r, r+N, ... of the job) and the decoded uint8 frames of all ranks are
+all-gathered once at the end of the timed loop (RCCL over xGMI, the only
+collective; the process group carries a timeout so a dead rank aborts the
+gather instead of hanging it).  `n_gpus` is the world size the process group
+reports.  Rank 0 prints ONE JSON line.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1|2|4]
 """
 import argparse
+import datetime
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
+import traceback
 
 import torch
 import torch.distributed as dist
@@ -27,12 +39,10 @@ import torch.distributed as dist
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from latentsync_amd import ops, shard  # noqa: E402
-from latentsync_amd.config import STAGE2_MODEL  # noqa: E402
-from latentsync_amd.pipeline import WindowEngine, load_fixed_mask  # noqa: E402
-from latentsync_amd.scheduler import DDIMScheduler  # noqa: E402
-from latentsync_amd.unet import UNet3DConditionModel  # noqa: E402
-from latentsync_amd.vae import AutoencoderKL  # noqa: E402
+# importing these does not touch the GPU (the HIP library loads on first use)
+from latentsync_amd import ops  # noqa: E402
+from latentsync_amd import unet as U  # noqa: E402
+from latentsync_amd.pipeline import load_fixed_mask  # noqa: E402
 
 SCHED_CFG = dict(beta_end=0.012, beta_schedule="scaled_linear", beta_start=0.00085, clip_sample=False,
                  num_train_timesteps=1000, set_alpha_to_one=False, steps_offset=1)  # configs/scheduler_config.json
@@ -42,7 +52,7 @@ PEAK_BF16_TF = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 # BASELINE.json configs this bench can run on one GPU (configs[0] is the CPU-only
 # plumbing case, configs[3] is configs[1] sharded over 8 ranks)
 # windows: independent 16-frame windows of a clip batched per UNet call (measured on MI355X:
-# 8 -> 110.2, 16 -> 113.3 frames/s at configs[1], gpurun_out/p23.log)
+# 8 -> 110.2, 16 -> 113.3 frames/s at configs[1], profiles/r01f_bench.json)
 PRESETS = {
     1: dict(resolution=256, guidance=1.0, steps=20, windows=16),
     2: dict(resolution=256, guidance=2.0, steps=50, windows=8),
@@ -191,114 +201,267 @@ def traffic_per_call():
     return round(json.load(open(p))["hbm_bytes_per_call"])
 
 
-def cpu_baseline(unet, vae, R=256, steps=20, Bu=1):
-    """The oracle (plain PyTorch fp32 restatement, oracle/ref_cpu.py) on host cores:
-    one full-size UNet forward at F=16 (B=1) + VAE encode/decode of one frame,
-    scaled to the window (steps x Bu UNet + 32 encodes + 16 decodes)."""
+def cpu_share():
+    """Host cores this process may actually use: the cgroup CPU quota when one is
+    set (the GPU box grants a 16-core share of a larger host whose
+    os.cpu_count() counts every core), else the affinity mask."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(p))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(unet, vae, R=256, steps=20, guidance=1.0, sample_steps=None):
+    """The oracle (plain PyTorch fp32 restatement, oracle/ref_cpu.py) on the host
+    cores: ONE full 16-frame window of the same configuration, end to end --
+    pixel prep, VAE encode x2 (16 frames each), `steps` UNet forwards (+CFG) with
+    the DDIM step, VAE decode of 16 frames, paste-back (oracle.pipeline_window).
+    Nothing is extrapolated when sample_steps is None; configs other than the
+    headline may pass a smaller sample_steps, and the sample text says so."""
     from oracle import ref_cpu as O
-    threads = min(16, os.cpu_count() or 1)
+    threads = cpu_share()
     torch.set_num_threads(threads)
     usd, vsd = unet._sd, vae._sd
-    g = torch.Generator().manual_seed(0)
-    h = R // 8
-    sample = torch.randn((1, 13, 16, h, h), generator=g)
-    audio = torch.randn((16, 50, 384), generator=g)
-    x = torch.rand((1, 3, R, R), generator=g) * 2 - 1
+    F, h = 16, R // 8
+    faces, audio, init, em, er = synthetic_window(F, R, h, unet.config.cross_attention_dim, 3, "cpu")
+    mask = load_fixed_mask(R)
+    n = steps if sample_steps is None else min(sample_steps, steps)
     with torch.no_grad():
         t0 = time.perf_counter()
-        O.unet_forward(usd, STAGE2_MODEL, sample, 951, audio)
-        t_unet = time.perf_counter() - t0
-        t0 = time.perf_counter()
-        O.vae_encode_moments(vsd, x)
-        t_enc = time.perf_counter() - t0
-        t0 = time.perf_counter()
-        O.vae_decode(vsd, torch.randn((1, 4, h, h), generator=g))
-        t_dec = time.perf_counter() - t0
-    t_window = steps * Bu * t_unet + 32 * t_enc + 16 * t_dec
-    return dict(value=16.0 / t_window, unit="frames/s", cores=threads, kind="port",
-                sample=f"{R}x{R}: 1 UNet fwd (B=1, F=16) {t_unet:.2f}s + 1-frame VAE enc {t_enc:.2f}s + dec "
-                       f"{t_dec:.2f}s, scaled to {steps}x{Bu} UNet + 32 enc + 16 dec per 16-frame window "
-                       "(oracle/ref_cpu.py fp32)")
+        O.pipeline_window(usd, dict(unet.config), vsd, faces, mask, audio, init, em, er, num_steps=n,
+                          guidance_scale=guidance)
+        t = time.perf_counter() - t0
+    if n == steps:
+        sample = (f"one full {R}x{R} 16-frame window, {steps} DDIM steps, guidance {guidance}: VAE enc x2 + "
+                  f"{steps} UNet fwd + DDIM + VAE dec + paste (oracle/ref_cpu.py pipeline_window, fp32) in {t:.1f} s")
+        value = F / t
+    else:
+        sample = (f"{R}x{R} 16-frame window with {n} of {steps} DDIM steps in {t:.1f} s; the UNet share scaled "
+                  f"to {steps} steps (extrapolated)")
+        value = F / (t * steps / n)
+    return dict(value=round(value, 5), unit="frames/s", cores=threads, kind="port", sample=sample,
+                window_s=round(t, 2), cpu_model=cpu_model(), os_cpu_count=os.cpu_count(),
+                threads_note="torch.set_num_threads(cgroup CPU share); os.cpu_count() counts the whole host")
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", type=int, default=1, choices=sorted(PRESETS),
-                    help="BASELINE.json configs[i]: 1 = 256^2/20 steps/g 1.0 (headline), 2 = 50 steps/g 2.0 (CFG), "
-                         "4 = 512^2/20 steps")
-    ap.add_argument("--guidance", type=float, default=None)
-    ap.add_argument("--inference-steps", type=int, default=None)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-graphs", action="store_true")
-    ap.add_argument("--windows-per-batch", type=int, default=None,
-                    help="independent 16-frame windows batched through one UNet call per DDIM step")
-    ap.add_argument("--no-single-window", action="store_true", help="skip the 1-window latency leg")
-    args = ap.parse_args()
-    pre = PRESETS[args.config]
-    if args.guidance is None:
-        args.guidance = pre["guidance"]
-    if args.inference_steps is None:
-        args.inference_steps = pre["steps"]
-    if args.windows_per_batch is None:
-        args.windows_per_batch = pre["windows"]
+def whisper_probe(device, seconds, seed=2):
+    """Audio2Feature.audio2feat + feature2chunks for one
+    clip of `seconds`, on the GPU (HIP events) and on the oracle (host cores).
+    Outside the headline's timed region; reported beside it (§8(d))."""
+    from latentsync_amd.audio import Audio2Feature
+    from oracle import ref_cpu as O
+    sr = 16000
+    wav = (torch.randn(int(seconds * sr), generator=torch.Generator().manual_seed(seed)) * 0.1).numpy()
+    a2f = Audio2Feature.random(seed, device=device)
+    for _ in range(2):  # warm-up (weights packed, kernels loaded)
+        a2f.feature2chunks(a2f._audio2feat(wav), 25)
+    torch.cuda.synchronize(device)
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    iters = 3
+    t0 = time.perf_counter()
+    e0.record(st)
+    for _ in range(iters):
+        chunks = a2f.feature2chunks(a2f._audio2feat(wav), 25)
+    e1.record(st)
+    torch.cuda.synchronize(device)
+    wall = (time.perf_counter() - t0) / iters
+    gpu_ms = e0.elapsed_time(e1) / iters
+    torch.set_num_threads(cpu_share())
+    filt = a2f._filters.cpu().float()
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        feat = O.whisper_features(a2f.sd, torch.from_numpy(wav), filt)
+        O.feature2chunks(feat)
+    cpu_s = time.perf_counter() - t0
+    return {"clip_s": seconds, "chunks": len(chunks), "gpu_ms": round(gpu_ms, 3), "gpu_wall_ms": round(wall * 1e3, 3),
+            "cpu_s": round(cpu_s, 3), "cpu_cores": cpu_share()}
 
+
+class PlumbingEngine:
+    """CPU stand-in for WindowEngine used by `--plumbing` (tests/test_bench_launch.py):
+    the same launcher, process group, window ownership and end-of-loop gather as
+    the GPU bench, with the window's compute replaced by writing the global window
+    index into its frames so the gathered clip order can be checked."""
+
+    def __init__(self, F, R, nw, rank, world):
+        self.F, self.R, self.nw, self.rank, self.world = F, R, nw, rank, world
+        self.out_u8 = torch.zeros((nw * F, R, R, 3), dtype=torch.uint8)
+        self.calls = 0
+
+    def run(self):
+        for k in range(self.nw):
+            local = self.calls * self.nw + k
+            self.out_u8[k * self.F:(k + 1) * self.F] = (self.rank + local * self.world) % 251
+        self.calls += 1
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(n):
+    """Spawn n fresh worker processes of this script, one per GPU, before anything
+    touches the GPU (the parent never initialises HIP).  A worker that fails ends
+    the job: the others (the exact processes started here) are terminated and the
+    first failure's status is returned."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
+def worker(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    if args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    plumbing = args.plumbing
+    if plumbing:
+        device = torch.device("cpu")
+    else:
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        kw = dict(rank=rank, world_size=world, timeout=datetime.timedelta(seconds=args.dist_timeout))
+        if plumbing:
+            dist.init_process_group("gloo", **kw)
+        else:
+            dist.init_process_group("nccl", device_id=device, **kw)
+        world = dist.get_world_size()  # n_gpus comes from the process group itself
+    from latentsync_amd import shard
 
-    F, R = 16, pre["resolution"]
+    F, R = 16, args.resolution
     h = R // 8
-    unet = UNet3DConditionModel(**STAGE2_MODEL).init_weights(41).to(device).eval()
-    vae = AutoencoderKL().init_weights(51).to(device)
-    sched = DDIMScheduler(**SCHED_CFG)
     nw = args.windows_per_batch
-    eng = WindowEngine(unet, vae, sched, F, R, args.inference_steps, args.guidance, use_graphs=not args.no_graphs,
-                       windows=nw)
-    faces, audio, init, em, er = synthetic_window(F * nw, R, h, unet.config.cross_attention_dim, 1000 + rank, device)
-    mask = load_fixed_mask(R).to(device)
-    eng.load(faces, mask, audio, init, em, er)
+    if plumbing:
+        eng = PlumbingEngine(F, R, nw, rank, world)
+        unet = vae = None
+    else:
+        from latentsync_amd.config import STAGE2_MODEL
+        from latentsync_amd.pipeline import WindowEngine
+        from latentsync_amd.scheduler import DDIMScheduler
+        from latentsync_amd.unet import UNet3DConditionModel
+        from latentsync_amd.vae import AutoencoderKL
+        unet = UNet3DConditionModel(**STAGE2_MODEL).init_weights(41).to(device).eval()
+        vae = AutoencoderKL().init_weights(51).to(device)
+        sched = DDIMScheduler(**SCHED_CFG)
+        eng = WindowEngine(unet, vae, sched, F, R, args.inference_steps, args.guidance,
+                           use_graphs=not args.no_graphs, windows=nw)
+        faces, audio, init, em, er = synthetic_window(F * nw, R, h, unet.config.cross_attention_dim, 1000 + rank,
+                                                      device)
+        mask = load_fixed_mask(R).to(device)
+        eng.load(faces, mask, audio, init, em, er)
+
+    def sync():
+        if not plumbing:
+            torch.cuda.synchronize(device)
 
     K, W = args.steps, args.warmup
     FB = F * nw  # frames per step (batch of windows)
     # rank r owns windows r, r+N, ... of the job (shard.rank_windows); K*nw per rank
     mine = torch.empty((K * nw, F, R, R, 3), dtype=torch.uint8, device=device)
-    for _ in range(max(W, 1) if not args.no_graphs else W):
+    for _ in range(max(W, 1) if not (args.no_graphs or plumbing) else W):
         eng.run()
-    torch.cuda.synchronize(device)
+    if plumbing:
+        eng.calls = 0
+    if args.fail_rank == rank:
+        raise RuntimeError(f"injected failure on rank {rank} (--fail-rank)")
+    if args.stall_rank == rank:
+        time.sleep(3600)  # a hung rank: the others' barrier / gather must time out
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(device)
-    stream = torch.cuda.current_stream()
+    sync()
     ev_step = []
     t0 = time.perf_counter()
     for k in range(K):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
+        if not plumbing:
+            st = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
         eng.run()
-        e1.record(stream)
-        ev_step.append((e0, e1))
+        if not plumbing:
+            e1.record(st)
+            ev_step.append((e0, e1))
         mine[k * nw:(k + 1) * nw].copy_(eng.out_u8.view(nw, F, R, R, 3))
     # decoded frames of every rank back in clip order: ONE all-gather over xGMI, at the end
     gathered = shard.gather_windows(mine, world * K * nw)
-    torch.cuda.synchronize(device)
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(device)
+    sync()
     elapsed = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    window_ms = sum(a.elapsed_time(b) for a, b in ev_step) / K
+    frames = world * K * FB
+    value = frames / elapsed
+    res = {
+        "metric": f"lip-synced frames/sec at {R}x{R}, 16-frame window, {args.inference_steps} DDIM steps",
+        "value": round(value, 3), "unit": "frames/s", "n_gpus": world, "steps": K, "warmup": W,
+        "ms_per_step": round(elapsed / K * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16", "data": "synthetic (seeded faces/audio/noise, random-init weights)",
+        "config": {"workload": f"configs[{args.config}]: {R}x{R} x16-frame windows, "
+                               f"{args.inference_steps} DDIM steps, guidance {args.guidance}, "
+                               "LatentSync-1.5 UNet + SD-VAE, bf16; "
+                               f"{nw} independent windows of a clip batched per UNet call",
+                   "windows_per_rank": K * nw, "windows_per_batch": nw, "frames_per_window": F,
+                   "global_batch": world * nw * F, "resolution": R,
+                   "parallelism": f"dp{world} (window sharding, RCCL all-gather of decoded frames)"},
+    }
+    if plumbing:
+        want = torch.arange(world * K * nw, dtype=torch.int64) % 251
+        got = gathered[:, 0, 0, 0, 0].to(torch.int64)
+        res["plumbing"] = {"backend": dist.get_backend() if world > 1 else "none",
+                           "gathered_windows": int(gathered.shape[0]),
+                           "clip_order_ok": bool(torch.equal(got, want)) and
+                           bool((gathered == gathered[:, :1, :1, :1, :1]).all())}
+        res["dtype"] = "u8"
+        if rank == 0:
+            print(json.dumps(res), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
+    window_ms = sum(a.elapsed_time(b) for a, b in ev_step) / K
     probe, attn_probe, blk_probe = step_probe(eng, device)
     single = None
     if rank == 0 and nw > 1 and not args.no_single_window:
@@ -317,51 +480,104 @@ def main():
     restore = None
     if rank == 0 and R == 256:
         restore = restore_probe(eng.out[:F].clone(), device)
-    frames = world * K * FB
-    value = frames / elapsed
     Bu = 2 if args.guidance > 1 else 1
     unet_tf, enc_tf, dec_tf = WORK_TF[R]
     tf_per_frame = (args.inference_steps * unet_tf * Bu + 32 * enc_tf + 16 * dec_tf) / 16
+    res.update({
+        "batch_ms_gpu_events": round(window_ms, 3),
+        "single_window": single,
+        "window_mfma_frac": round(tf_per_frame * value / world / PEAK_BF16_TF, 4),
+        "roofline": {"bound": "mfma",
+                     "kernel": "conv_gemm family: every ls_conv2d call of one UNet fwd (conv_gemm_* tiled / "
+                               "gemm_rowblock GEMM + split-K reduce)",
+                     "achieved": round(probe["tflops"], 2), "peak": PEAK_BF16_TF, "unit": "TFLOP/s",
+                     "frac": round(probe["tflops"] / PEAK_BF16_TF, 4), "traffic": traffic_per_call(),
+                     "traffic_unit": "HBM bytes per ls_conv2d call (rocprofv3 PMC, profiles/pmc_traffic.json)",
+                     "launches": probe["launches"], "avg_launch_ms": round(probe["avg_ms"], 4),
+                     "flops_per_launch": probe["flops_per_launch"],
+                     "algorithmic_bytes_per_launch": round(probe["algo_bytes_per_launch"]),
+                     "peak_measured": measured_peak()},
+        "attention": {"kernel": "ls_attention (SDPA: spatial self, audio cross, temporal)",
+                      "achieved_tflops": round(attn_probe["tflops"], 2), "launches": attn_probe["launches"],
+                      "avg_launch_ms": round(attn_probe["avg_ms"], 4),
+                      "frac": round(attn_probe["tflops"] / PEAK_BF16_TF, 4),
+                      "blocks": "Transformer3DModel + motion modules (a14-a17): GEMM + SDPA FLOPs / block wall time",
+                      "blocks_tflops": round(blk_probe["tflops"], 2), "blocks_n": blk_probe["launches"],
+                      "blocks_ms": round(blk_probe["total_ms"], 3),
+                      "blocks_mfma_frac": round(blk_probe["tflops"] / PEAK_BF16_TF, 4)},
+        "restore_video": restore,
+    })
+    if rank == 0 and not args.no_whisper:
+        # Whisper features for the clip of one step's frames (FB frames at 25 fps),
+        # outside the headline; value_incl_whisper adds one clip's feature time per step
+        wp = whisper_probe(device, FB / 25.0)
+        res["whisper"] = wp
+        res["value_incl_whisper"] = round(frames / (elapsed + K * wp["gpu_wall_ms"] * 1e-3), 3)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sample_steps = None if args.config == 1 else 2
+        res["cpu_baseline"] = cpu_baseline(unet, vae, R, args.inference_steps, args.guidance, sample_steps)
+        res["speedup_vs_cpu"] = round(value / res["cpu_baseline"]["value"], 1)
     if rank == 0:
-        res = {
-            "metric": f"lip-synced frames/sec at {R}x{R}, 16-frame window, {args.inference_steps} DDIM steps",
-            "value": round(value, 3), "unit": "frames/s", "n_gpus": world, "steps": K, "warmup": W,
-            "ms_per_step": round(elapsed / K * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16", "data": "synthetic (seeded faces/audio/noise, random-init weights)",
-            "config": {"workload": f"configs[{args.config}]: {R}x{R} x16-frame windows, "
-                                   f"{args.inference_steps} DDIM steps, guidance {args.guidance}, "
-                                   "LatentSync-1.5 UNet + SD-VAE, bf16; "
-                                   f"{nw} independent windows of a clip batched per UNet call",
-                       "windows_per_rank": K * nw, "windows_per_batch": nw, "frames_per_window": F,
-                       "global_batch": world * nw * F, "resolution": R,
-                       "parallelism": f"dp{world} (window sharding, RCCL all-gather of decoded frames)"},
-            "batch_ms_gpu_events": round(window_ms, 3),
-            "single_window": single,
-            "window_mfma_frac": round(tf_per_frame * value / world / PEAK_BF16_TF, 4),
-            "roofline": {"bound": "mfma",
-                         "kernel": "conv_gemm family: every ls_conv2d call of one UNet fwd (conv_gemm_* tiled / gemm_rowblock GEMM + split-K reduce)",
-                         "achieved": round(probe["tflops"], 2), "peak": PEAK_BF16_TF, "unit": "TFLOP/s",
-                         "frac": round(probe["tflops"] / PEAK_BF16_TF, 4), "traffic": traffic_per_call(),
-                         "traffic_unit": "HBM bytes per ls_conv2d call (rocprofv3 PMC, profiles/pmc_traffic.json)",
-                         "launches": probe["launches"], "avg_launch_ms": round(probe["avg_ms"], 4),
-                         "flops_per_launch": probe["flops_per_launch"],
-                         "algorithmic_bytes_per_launch": round(probe["algo_bytes_per_launch"])},
-            "attention": {"kernel": "ls_attention (SDPA: spatial self, audio cross, temporal)",
-                          "achieved_tflops": round(attn_probe["tflops"], 2), "launches": attn_probe["launches"],
-                          "avg_launch_ms": round(attn_probe["avg_ms"], 4),
-                          "frac": round(attn_probe["tflops"] / PEAK_BF16_TF, 4),
-                          "blocks": "Transformer3DModel + motion modules (a14-a17): GEMM + SDPA FLOPs / block wall time",
-                          "blocks_tflops": round(blk_probe["tflops"], 2), "blocks_n": blk_probe["launches"],
-                          "blocks_ms": round(blk_probe["total_ms"], 3),
-                          "blocks_mfma_frac": round(blk_probe["tflops"] / PEAK_BF16_TF, 4)},
-            "restore_video": restore,
-        }
-        if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(unet, vae, R, args.inference_steps, Bu)
-            res["speedup_vs_cpu"] = round(value / res["cpu_baseline"]["value"], 1)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def measured_peak():
+    """Measured dense bf16 GEMM ceiling on the box (scripts/gemm_ceiling.py ->
+    profiles/gemm_ceiling.json), or None before it has been measured."""
+    p = os.path.join(REPO, "profiles", "gemm_ceiling.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        return json.load(f).get("best_tflops")
+
+
+def parse_args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", type=int, default=1, choices=sorted(PRESETS),
+                    help="BASELINE.json configs[i]: 1 = 256^2/20 steps/g 1.0 (headline), 2 = 50 steps/g 2.0 (CFG), "
+                         "4 = 512^2/20 steps")
+    ap.add_argument("--guidance", type=float, default=None)
+    ap.add_argument("--inference-steps", type=int, default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-whisper", action="store_true")
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--windows-per-batch", type=int, default=None,
+                    help="independent 16-frame windows batched through one UNet call per DDIM step")
+    ap.add_argument("--no-single-window", action="store_true", help="skip the 1-window latency leg")
+    ap.add_argument("--dist-timeout", type=float, default=300.0,
+                    help="process-group timeout (s): a rank that dies aborts the others' collectives")
+    ap.add_argument("--plumbing", action="store_true",
+                    help="CPU/gloo dry run of the launcher, window sharding and gather (no GPU)")
+    ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--stall-rank", type=int, default=-1, help=argparse.SUPPRESS)
+    args = ap.parse_args()
+    pre = PRESETS[args.config]
+    if args.guidance is None:
+        args.guidance = pre["guidance"]
+    if args.inference_steps is None:
+        args.inference_steps = pre["steps"]
+    if args.windows_per_batch is None:
+        args.windows_per_batch = pre["windows"] if not args.plumbing else 2
+    args.resolution = pre["resolution"] if not args.plumbing else 8
+    return args
+
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args.gpus))
+    try:
+        worker(args)
+    except BaseException:
+        rank = os.environ.get("RANK", "0")
+        sys.stderr.write(f"[bench rank {rank}] failed:\n{traceback.format_exc()}")
+        sys.stderr.flush()
+        os._exit(1)  # no destructor waits on peers that may be blocked in a collective
 
 
 if __name__ == "__main__":

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LS_ABI_VERSION 5
+#define LS_ABI_VERSION 6
 
 typedef enum {
   LS_OK = 0,
@@ -291,6 +291,30 @@ size_t ls_restore_workspace_bytes(int32_t N, int32_t roi_h, int32_t roi_w);
 int ls_restore_frames(uint8_t* frames, int32_t N, int32_t H, int32_t W, const uint8_t* faces, int32_t fh, int32_t fw,
                       const double* warp, const int32_t* roi, int32_t roi_h, int32_t roi_w, int32_t w_edge_max,
                       const void* tables, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---- face-alignment ingest + mask resize, SURVEY.md §8(f) row 2 / §8(a) a3 ----------- */
+
+/* cv2.resize(img, (dst_w, dst_h), interpolation=INTER_LANCZOS4) for N uint8 HWC images
+ * with C (1..4) interleaved channels: load_fixed_mask's mask.png resize
+ * (image_processor.py:31-36) and the aligned face's resize to the resolution
+ * (image_processor.py:141).  OpenCV's generic resize path (resize.cpp resizeGeneric_
+ * with HResizeLanczos4 / VResizeLanczos4: int16 coefficients saturate_cast(c * 2048),
+ * taps clamped to the image, (sum + 2^21) >> 22); dst_h == src_h and dst_w == src_w is
+ * a copy, as in cv::resize.  The per-axis tables are built on the host and copied into
+ * `workspace` (ls_resize_lanczos4_workspace_bytes): this call synchronises `stream`
+ * (one-off preprocessing; not capturable). */
+size_t ls_resize_lanczos4_workspace_bytes(int32_t dst_h, int32_t dst_w);
+int ls_resize_lanczos4_u8(const uint8_t* src, int32_t N, int32_t src_h, int32_t src_w, int32_t C, uint8_t* dst,
+                          int32_t dst_h, int32_t dst_w, void* workspace, size_t workspace_bytes, void* stream);
+
+/* AlignRestore.align_warp_face (affine_transform.py:53-70): cv2.warpAffine(frame, M,
+ * (out_w, out_h), INTER_LANCZOS4, BORDER_CONSTANT, border_value) for N uint8 RGB
+ * frames [N][H][W][3] -> out [N][out_h][out_w][3].  warp fp64 [N][6] is the
+ * dst->src matrix warpAffine iterates with (the inverse of M, in warpAffine's own
+ * operation order); tables = the buffer of ls_restore_init_tables (its Lanczos-4
+ * table). */
+int ls_align_warp_u8(const uint8_t* frames, int32_t N, int32_t H, int32_t W, const double* warp, int32_t out_h,
+                     int32_t out_w, int32_t border_value, const void* tables, uint8_t* out, void* stream);
 
 int ls_abi_version(void);
 const char* ls_last_error(void);

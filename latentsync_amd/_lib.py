@@ -10,7 +10,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LS_HIP_LIB", os.path.join(HERE, "libls_hip.so"))
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 c_u16p = C.c_void_p
 c_vp = C.c_void_p
@@ -84,6 +84,11 @@ _SIGS = {
     "ls_restore_workspace_bytes": (C.c_size_t, [C.c_int32, C.c_int32, C.c_int32]),
     "ls_restore_frames": (C.c_int, [c_vp, C.c_int32, C.c_int32, C.c_int32, c_vp, C.c_int32, C.c_int32, c_vp, c_vp,
                                     C.c_int32, C.c_int32, C.c_int32, c_vp, c_vp, C.c_size_t, c_vp]),
+    "ls_resize_lanczos4_workspace_bytes": (C.c_size_t, [C.c_int32, C.c_int32]),
+    "ls_resize_lanczos4_u8": (C.c_int, [c_vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, c_vp, C.c_int32, C.c_int32,
+                                        c_vp, C.c_size_t, c_vp]),
+    "ls_align_warp_u8": (C.c_int, [c_vp, C.c_int32, C.c_int32, C.c_int32, c_vp, C.c_int32, C.c_int32, C.c_int32,
+                                   c_vp, c_vp, c_vp]),
     "ls_add_rows": (C.c_int, [c_vp, C.c_int64, C.c_int32, C.c_int32, c_vp, C.c_int32, c_vp, C.c_int32, c_vp]),
 }
 

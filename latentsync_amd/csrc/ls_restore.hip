@@ -422,6 +422,121 @@ __global__ void __launch_bounds__(256) blur_cols_blend_kernel(
   }
 }
 
+// ---------------------------------------------------------------- cv2.resize INTER_LANCZOS4
+// resize.cpp's own interpolateLanczos4 (no FLT_EPSILON guard: x ~ 0 is caught by the
+// 1e30 centre tap); (x + 3) and (x + 3 - i) are float sums, as in the C++ source.
+static void resize_lanczos4_coeffs(float x, float* c) {
+  const double s45 = 0.70710678118654752440084436210485;
+  const double cs[8][2] = {{1, 0}, {-s45, -s45}, {0, 1}, {s45, -s45}, {-1, 0}, {s45, s45}, {0, -1}, {-s45, s45}};
+  const float x3 = x + 3.f;
+  const double y0 = ((double)(-x3) * M_PI) * 0.25, s0 = std::sin(y0), c0 = std::cos(y0);
+  float sum = 0.f;
+  for (int i = 0; i < 8; ++i) {
+    const float yy = x3 - (float)i;
+    if (std::fabs(yy) >= 1e-6f) {
+      const double y = ((double)(-yy) * M_PI) * 0.25;
+      c[i] = (float)((cs[i][0] * s0 + cs[i][1] * c0) / (y * y));
+    } else {
+      c[i] = 1e30f;
+    }
+    sum += c[i];
+  }
+  const float inv = 1.f / sum;
+  for (int i = 0; i < 8; ++i) c[i] *= inv;
+}
+
+// resizeGeneric_ per-axis tables: f = (float)((d + 0.5) * scale - 0.5), s = floor(f),
+// scale = 1 / (dst / src) in double; 8 int16 coefficients saturate_cast(c * 2048).
+static void resize_axis(int sn, int dn, int32_t* ofs, int16_t* coef) {
+  const double inv_scale = (double)dn / sn, scale = 1. / inv_scale;
+  for (int d = 0; d < dn; ++d) {
+    float f = (float)((d + 0.5) * scale - 0.5);
+    const int s = (int)std::floor(f);
+    f -= (float)s;
+    float c[8];
+    resize_lanczos4_coeffs(f, c);
+    ofs[d] = s;
+    for (int k = 0; k < 8; ++k) {
+      long r = std::lrint(c[k] * 2048.f);
+      coef[d * 8 + k] = (int16_t)(r < -32768 ? -32768 : (r > 32767 ? 32767 : r));
+    }
+  }
+}
+
+// HResizeLanczos4 (int row sums of u8 * int16, taps clamped to the row) then
+// VResizeLanczos4 (int sums of the 8 clamped rows * int16) and
+// FixedPtCast<int, uchar, 22>: (v + 2^21) >> 22, saturated.
+__global__ void __launch_bounds__(256) resize_lanczos4_kernel(const uint8_t* __restrict__ src, int sh, int sw, int C,
+                                                              uint8_t* __restrict__ dst, int dh, int dw,
+                                                              const int32_t* __restrict__ ofs_x,
+                                                              const int32_t* __restrict__ ofs_y,
+                                                              const int16_t* __restrict__ ax,
+                                                              const int16_t* __restrict__ ay) {
+  const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int n = blockIdx.z;
+  if (x >= dw || y >= dh) return;
+  const int sx = ofs_x[x] - 3, sy = ofs_y[y] - 3;
+  int xi[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) xi[j] = min(max(sx + j, 0), sw - 1) * C;
+  const uint8_t* img = src + (long)n * sh * sw * C;
+  int acc[4] = {0, 0, 0, 0};
+  for (int k = 0; k < 8; ++k) {
+    const uint8_t* row = img + (long)min(max(sy + k, 0), sh - 1) * sw * C;
+    const int b = ay[y * 8 + k];
+    for (int c = 0; c < C; ++c) {
+      int h = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) h += (int)row[xi[j] + c] * (int)ax[x * 8 + j];
+      acc[c] += h * b;
+    }
+  }
+  uint8_t* o = dst + (((long)n * dh + y) * dw + x) * C;
+  for (int c = 0; c < C; ++c) o[c] = (uint8_t)min(max((acc[c] + (1 << 21)) >> 22, 0), 255);
+}
+
+// cv2.warpAffine(frame, M, (out_w, out_h), INTER_LANCZOS4, BORDER_CONSTANT, border) --
+// AlignRestore.align_warp_face (affine_transform.py:53-70).  remapLanczos4 fixed point:
+// sum = border 2^15 + sum over in-image taps (S - border) w, i.e. taps outside read the
+// border value (the 64 taps sum to exactly 2^15); (sum + 2^14) >> 15 saturated.
+__global__ void __launch_bounds__(256) align_warp_kernel(const uint8_t* __restrict__ frames, int H, int W,
+                                                         const double* __restrict__ warp,
+                                                         const int16_t* __restrict__ ltab, int oh, int ow,
+                                                         int border, uint8_t* __restrict__ out) {
+  const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int n = blockIdx.z;
+  if (x >= ow || y >= oh) return;
+  const WarpPt p = warp_point(warp + 6 * n, x, y);
+  const int sx = p.sx - 3, sy = p.sy - 3;
+  const int16_t* w = ltab + p.fxy * 64;
+  const uint8_t* fr = frames + (long)n * H * W * 3;
+  int acc[3] = {0, 0, 0};
+  for (int rr = 0; rr < 8; ++rr) {
+    const int yy = sy + rr;
+    const bool rin = (unsigned)yy < (unsigned)H;
+#pragma unroll
+    for (int cc = 0; cc < 8; ++cc) {
+      const int xx = sx + cc;
+      const int ww = w[rr * 8 + cc];
+      if (rin && (unsigned)xx < (unsigned)W) {
+        const uint8_t* px = fr + ((long)yy * W + xx) * 3;
+        acc[0] += px[0] * ww;
+        acc[1] += px[1] * ww;
+        acc[2] += px[2] * ww;
+      } else {
+        acc[0] += border * ww;
+        acc[1] += border * ww;
+        acc[2] += border * ww;
+      }
+    }
+  }
+  uint8_t* o = out + (((long)n * oh + y) * ow + x) * 3;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) o[c] = (uint8_t)min(max((acc[c] + (1 << 14)) >> 15, 0), 255);
+}
+
 static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 }  // namespace ls
@@ -495,6 +610,53 @@ int ls_restore_frames(uint8_t* frames, int32_t N, int32_t H, int32_t W, const ui
   hipLaunchKernelGGL(blur_cols_blend_kernel, grid, blk, 0, s, tmp, mask_e, roi, area, gtab, w_edge_max, warp, faces,
                      fh, fw, ltab, H, W, roi_w, roi_h, frames);
   return check_launch("ls_restore_frames");
+}
+
+size_t ls_resize_lanczos4_workspace_bytes(int32_t dst_h, int32_t dst_w) {
+  if (dst_h <= 0 || dst_w <= 0) return 0;
+  return align256(sizeof(int32_t) * (size_t)(dst_h + dst_w)) + align256(16 * (size_t)(dst_h + dst_w));
+}
+
+int ls_resize_lanczos4_u8(const uint8_t* src, int32_t N, int32_t src_h, int32_t src_w, int32_t C, uint8_t* dst,
+                          int32_t dst_h, int32_t dst_w, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!src || !dst || N < 0 || src_h <= 0 || src_w <= 0 || dst_h <= 0 || dst_w <= 0 || C < 1 || C > 4)
+    return fail(LS_ERR_INVALID, "ls_resize_lanczos4_u8: bad args (C in 1..4)");
+  hipStream_t s = (hipStream_t)stream;
+  if (N == 0) return LS_OK;
+  if (src_h == dst_h && src_w == dst_w) {  // cv::resize copies when dsize == ssize
+    if (hipMemcpyAsync(dst, src, (size_t)N * src_h * src_w * C, hipMemcpyDeviceToDevice, s) != hipSuccess)
+      return fail(LS_ERR_LAUNCH, "ls_resize_lanczos4_u8: copy failed");
+    return LS_OK;
+  }
+  const size_t need = ls_resize_lanczos4_workspace_bytes(dst_h, dst_w);
+  if (!workspace || workspace_bytes < need) return fail(LS_ERR_WORKSPACE, "ls_resize_lanczos4_u8: workspace");
+  std::vector<uint8_t> host(need, 0);
+  int32_t* ofs_x = (int32_t*)host.data();
+  int32_t* ofs_y = ofs_x + dst_w;
+  int16_t* ax = (int16_t*)(host.data() + align256(sizeof(int32_t) * (size_t)(dst_h + dst_w)));
+  int16_t* ay = ax + 8 * (size_t)dst_w;
+  resize_axis(src_w, dst_w, ofs_x, ax);
+  resize_axis(src_h, dst_h, ofs_y, ay);
+  if (hipMemcpyAsync(workspace, host.data(), need, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return fail(LS_ERR_LAUNCH, "ls_resize_lanczos4_u8: table copy failed");
+  const uint8_t* ws = (const uint8_t*)workspace;
+  const int32_t* d_ofs_x = (const int32_t*)ws;
+  const int16_t* d_ax = (const int16_t*)(ws + ((const uint8_t*)ax - host.data()));
+  hipLaunchKernelGGL(resize_lanczos4_kernel, dim3(cdiv(dst_w, 64), cdiv(dst_h, 4), N), dim3(256), 0, s, src, src_h,
+                     src_w, C, dst, dst_h, dst_w, d_ofs_x, d_ofs_x + dst_w, d_ax, d_ax + 8 * (size_t)dst_w);
+  return check_launch("resize_lanczos4_kernel");
+}
+
+int ls_align_warp_u8(const uint8_t* frames, int32_t N, int32_t H, int32_t W, const double* warp, int32_t out_h,
+                     int32_t out_w, int32_t border_value, const void* tables, uint8_t* out, void* stream) {
+  if (!frames || !warp || !tables || !out || N < 0 || H <= 0 || W <= 0 || out_h <= 0 || out_w <= 0 ||
+      border_value < 0 || border_value > 255)
+    return fail(LS_ERR_INVALID, "ls_align_warp_u8: bad args");
+  if (N == 0) return LS_OK;
+  hipLaunchKernelGGL(align_warp_kernel, dim3(cdiv(out_w, 64), cdiv(out_h, 4), N), dim3(256), 0, (hipStream_t)stream,
+                     frames, H, W, warp, (const int16_t*)tables, out_h, out_w, border_value, out);
+  return check_launch("align_warp_kernel");
 }
 
 }  // extern "C"

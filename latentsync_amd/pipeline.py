@@ -30,22 +30,27 @@ from . import ops, shard
 SCALING = 0.18215
 
 
-def load_fixed_mask(resolution=256, mask_image_path=None):
+def load_fixed_mask(resolution=256, mask_image_path=None, device=None):
     """load_fixed_mask (image_processor.py:31-36) -> keep-mask (R, R) float32,
-    1 = keep the original pixel, 0 = mouth region to regenerate."""
+    1 = keep the original pixel, 0 = mouth region to regenerate.  The uint8 mask
+    image (the reference's mask.png, 256^2, shipped as packed bits) is resized
+    with cv2's INTER_LANCZOS4 arithmetic on the device (ls_resize_lanczos4_u8) when
+    the resolution differs -- fractional edge values k/255, as the reference gets --
+    then divided by 255.  All channels of the gray mask are equal, so one is resized
+    (the reference keeps channel 0 for the UNet mask, :152)."""
     if mask_image_path is None or not os.path.exists(mask_image_path):
         bits = np.load(os.path.join(os.path.dirname(__file__), "assets", "fix_mask_256.npz"))["bits"]
-        m = np.unpackbits(bits)[: 256 * 256].reshape(256, 256).astype(np.float32)
+        m8 = (np.unpackbits(bits)[: 256 * 256].reshape(256, 256) * 255).astype(np.uint8)
     else:
         from PIL import Image
-        img = np.array(Image.open(mask_image_path).convert("RGB"))
-        m = (img[..., 0].astype(np.float64) / 255.0).astype(np.float32)
-    t = torch.from_numpy(m)
-    if t.shape[0] != resolution:
-        if resolution % t.shape[0] and t.shape[0] % resolution:
-            raise NotImplementedError("mask resize needs cv2 LANCZOS (out of scope); use a mask at the resolution")
-        t = torch.nn.functional.interpolate(t[None, None], size=(resolution, resolution), mode="nearest")[0, 0]
-    return t
+        m8 = np.array(Image.open(mask_image_path).convert("RGB"))[..., 0].copy()
+    t = torch.from_numpy(m8)
+    if tuple(t.shape) != (resolution, resolution):
+        from .align import resize_lanczos4
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        t = resize_lanczos4(t.to(dev), resolution, resolution)
+    t = (t.to(torch.float64) / 255.0).to(torch.float32)
+    return t.to(device) if device is not None else t.cpu()
 
 
 def load_data_pth(data_path):
@@ -184,22 +189,27 @@ class WindowEngine:
         self.eps_m.copy_(eps_masked.float().permute(0, 2, 3, 1).reshape(-1, 4))
         self.eps_r.copy_(eps_ref.float().permute(0, 2, 3, 1).reshape(-1, 4))
 
-    def run(self):
+    def latents(self):
+        """The DDIM state as the reference holds it: (windows, 4, F, h, w) fp32 view."""
+        h = self.h
+        return self.lat.view(self.nw, self.F, h, h, 4).permute(0, 4, 1, 2, 3)
+
+    def run(self, callback=None, callback_steps=1):
         """Execute the staged window; results in self.out (F,3,R,R) fp32 and
-        self.out_u8 (F,R,R,3)."""
-        if self.use_graphs:
-            if self.graphs is None:
-                self.capture()
-            g_enc, g_step, g_dec = self.graphs
-            g_enc.replay()
-            for _ in range(self.steps):
-                g_step.replay()
-            g_dec.replay()
-        else:
-            self._encode()
-            for _ in range(self.steps):
-                self._step()
-            self._decode()
+        self.out_u8 (F,R,R,3).  ``callback(j, t, latents)`` is called after DDIM
+        step j when j % callback_steps == 0, as lipsync_pipeline.py:564-568 does
+        (scheduler.order == 1, so no warm-up steps); the step graph is then
+        replayed one step at a time with the host call in between."""
+        if self.use_graphs and self.graphs is None:
+            self.capture()
+        enc, step, dec = ((g.replay for g in self.graphs) if self.use_graphs
+                          else (self._encode, self._step, self._decode))
+        enc()
+        for j in range(self.steps):
+            step()
+            if callback is not None and j % callback_steps == 0:
+                callback(j, self.scheduler.timesteps[j], self.latents())
+        dec()
         return self.out
 
 
@@ -260,20 +270,22 @@ class LipsyncPipeline:
                     generator=None, all_latents=None, vae_noise=None, callback=None, callback_steps=1):
         """The hot loop (:489-575) over ceil(len(chunks)/num_frames) windows.
         faces_u8 (N,3,R,R) (N >= #chunks, already repeated/truncated as the
-        reference does), whisper_chunks (N,50,384).  Returns decoded + pasted
-        frames (N', 3, R, R) fp32 and uint8 (N', R, R, 3) on device."""
+        reference does), whisper_chunks (n,50,384).  Window i covers frames
+        [i*num_frames, (i+1)*num_frames) of the n chunks; the last one is short
+        when n % num_frames != 0 (force_video_length, :455, :500-511) and runs
+        with its own frame count, as the reference's slices do.  Returns decoded +
+        pasted frames (n, 3, R, R) fp32 and uint8 (n, R, R, 3) on device."""
         R = faces_u8.shape[-1]
         self.check_inputs(R, R, callback_steps)
         n = whisper_chunks.shape[0]
+        if faces_u8.shape[0] < n:
+            raise ValueError(f"{faces_u8.shape[0]} faces for {n} audio chunks: repeat the faces first (:448-452)")
         if all_latents is None:
             all_latents = self.prepare_latents(n, R, R, generator)
         h = R // self.vae_scale_factor
-        outs, outs_u8 = [], []
         mask = mask.to(self.device, torch.float32)
         n_inf = math.ceil(n / num_frames)
-        if n % num_frames:
-            raise ValueError("the last window is short: pad the chunks to a multiple of num_frames "
-                             "(pad_whisper_chunks_end, as the reference does)")
+        size = [min(num_frames, n - i * num_frames) for i in range(n_inf)]
         # With torch.distributed initialised, rank r runs windows r, r+W, ... and the
         # decoded frames are all-gathered once at the end (shard.py).  Every rank
         # still draws every window's VAE noise so the result is independent of W.
@@ -284,31 +296,42 @@ class LipsyncPipeline:
             if vae_noise is not None:
                 noise[i] = vae_noise(i)
             else:
-                noise[i] = (torch.randn((num_frames, 4, h, h), generator=generator, device=self.device),
-                            torch.randn((num_frames, 4, h, h), generator=generator, device=self.device))
-        # `windows_per_batch` of this rank's windows go through one UNet call per step
-        nb = max(1, int(self.windows_per_batch))
-        for b0 in range(0, len(mine), nb):
-            wins = mine[b0:b0 + nb]
-            eng = self.engine(num_frames, R, num_inference_steps, guidance_scale, windows=len(wins))
-            sls = [slice(i * num_frames, (i + 1) * num_frames) for i in wins]
+                noise[i] = (torch.randn((size[i], 4, h, h), generator=generator, device=self.device),
+                            torch.randn((size[i], 4, h, h), generator=generator, device=self.device))
+        # `windows_per_batch` full windows go through one UNet call per step; a short
+        # last window runs alone (eagerly: it happens once per clip).  A per-step
+        # callback sees one window's latents at a time, as in the reference.
+        nb = 1 if callback is not None else max(1, int(self.windows_per_batch))
+        full = [i for i in mine if size[i] == num_frames]
+        batches = [full[b:b + nb] for b in range(0, len(full), nb)] + [[i] for i in mine if size[i] < num_frames]
+        res = {}
+        for wins in batches:
+            Fw = size[wins[0]]
+            eng = self.engine(Fw, R, num_inference_steps, guidance_scale, use_graphs=Fw == num_frames,
+                              windows=len(wins))
+            sls = [slice(i * num_frames, i * num_frames + Fw) for i in wins]
             cat = lambda xs: torch.cat([x.to(self.device) for x in xs])
             eng.load(cat([faces_u8[sl] for sl in sls]), mask, cat([whisper_chunks[sl] for sl in sls]),
                      cat([all_latents[:, :, sl] for sl in sls]),
                      cat([noise[i][0] for i in wins]), cat([noise[i][1] for i in wins]))
-            eng.run()
+            eng.run(callback=callback, callback_steps=callback_steps)
             for k, i in enumerate(wins):
-                fs = slice(k * num_frames, (k + 1) * num_frames)
-                outs.append(eng.out[fs].clone())
-                outs_u8.append(eng.out_u8[fs].clone())
-                if callback is not None:
-                    callback(i, None, eng.lat)
+                fs = slice(k * Fw, (k + 1) * Fw)
+                res[i] = (eng.out[fs].clone(), eng.out_u8[fs].clone())
         if world == 1:
-            return torch.cat(outs), torch.cat(outs_u8)
+            return torch.cat([res[i][0] for i in mine]), torch.cat([res[i][1] for i in mine])
+        # one all-gather of equally sized slabs: a short window is zero-padded to
+        # num_frames for the exchange and the padding dropped after it
         F_, dev = num_frames, self.device
-        loc = torch.stack(outs) if outs else torch.empty((0, F_, 3, R, R), device=dev)
-        loc8 = torch.stack(outs_u8) if outs_u8 else torch.empty((0, F_, R, R, 3), dtype=torch.uint8, device=dev)
-        return (shard.gather_windows(loc, n_inf).flatten(0, 1), shard.gather_windows(loc8, n_inf).flatten(0, 1))
+
+        def padded(t):
+            if t.shape[0] == F_:
+                return t
+            return torch.cat([t, t.new_zeros((F_ - t.shape[0],) + tuple(t.shape[1:]))])
+        loc = torch.stack([padded(res[i][0]) for i in mine]) if mine else torch.empty((0, F_, 3, R, R), device=dev)
+        loc8 = torch.stack([padded(res[i][1]) for i in mine]) if mine else \
+            torch.empty((0, F_, R, R, 3), dtype=torch.uint8, device=dev)
+        return (shard.gather_windows(loc, n_inf).flatten(0, 1)[:n], shard.gather_windows(loc8, n_inf).flatten(0, 1)[:n])
 
     def restore_video(self, faces, video_frames, boxes, affine_matrices):
         """:343-358 on the device (latentsync_amd/restore.py): every face of the clip
@@ -343,7 +366,10 @@ class LipsyncPipeline:
         if not data_path:
             raise NotImplementedError("face detection / alignment is out of scope: pass data_path (.pth)")
         data = load_data_pth(data_path)
-        faces = data["faces"]
+        faces, boxes, affine_matrices = data["faces"], list(data["boxes"]), list(data["affine_matrices"])
+        # the original frames are read up front (:405) because they are repeated /
+        # truncated together with the faces, boxes and matrices below
+        video_frames = None if kwargs.get("faces_only") else read_video_frames(video_path)
         R = height or faces.shape[-1]
         self.check_inputs(R, width or R, callback_steps)
         if faces.shape[-1] != R:
@@ -355,6 +381,14 @@ class LipsyncPipeline:
         chunks = self.audio_encoder.feature2chunks(feature_array=feat, fps=video_fps)
         shape = chunks[0].shape
         padding_duration = 0.0
+
+        def per_frame(fn, n):
+            """Apply a repeat/truncate to every per-frame sequence together (:448-452, :462-466)."""
+            nonlocal faces, boxes, affine_matrices, video_frames
+            faces, boxes, affine_matrices = fn(faces, n), fn(boxes, n), fn(affine_matrices, n)
+            if video_frames is not None:
+                video_frames = fn(video_frames, n)
+
         if not force_video_length:
             if start_from_backwards:
                 chunks, audio_samples, padding_duration, _ = rep.pad_whisper_chunks(chunks, shape, audio_samples,
@@ -363,21 +397,20 @@ class LipsyncPipeline:
                 chunks, audio_samples, padding_duration = rep.pad_whisper_chunks_end(chunks, shape, audio_samples,
                                                                                      audio_sample_rate, video_fps)
             if len(chunks) > len(faces):
-                faces = rep.repeat_to_length(faces, len(chunks))
+                per_frame(rep.repeat_to_length, len(chunks))
         else:
             chunks, audio_samples, padding_duration = rep.pad_whisper_chunks_to_target(
                 chunks, shape, audio_samples, audio_sample_rate, len(faces), fps=video_fps)
         if len(faces) != len(chunks) and start_from_backwards:
-            faces = rep.truncate_to_length(faces, len(chunks))
+            per_frame(rep.truncate_to_length, len(chunks))
         chunks = torch.stack([c.to(self.device) for c in chunks])
         out, out_u8 = self.run_windows(faces, chunks, keep, num_frames, num_inference_steps, guidance_scale,
                                        generator, callback=callback, callback_steps=callback_steps)
         if shard.world_and_rank()[1] != 0:
             return None  # every rank holds the gathered clip; rank 0 restores and writes it
         frames_out = out_u8
-        video_frames = None if kwargs.get("faces_only") else read_video_frames(video_path)
         if video_frames is not None:
-            frames_out = self.restore_video(out, video_frames, data["boxes"], data["affine_matrices"])
+            frames_out = self.restore_video(out, video_frames, boxes, affine_matrices)
         n_out = frames_out.shape[0]
         audio_keep = int(n_out / video_fps * audio_sample_rate)
         np.savez(video_out_path if video_out_path.endswith(".npz") else video_out_path + ".npz",

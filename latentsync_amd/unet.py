@@ -546,7 +546,18 @@ class UNet3DConditionModel(torch.nn.Module):
             sample = 2 * sample - 1.0
         x = torch.zeros((B * F, H, W, dev.cin_pad), dtype=torch.bfloat16, device=sample.device)
         x[..., :Cin] = sample.permute(0, 2, 3, 4, 1).reshape(B * F, H, W, Cin)
-        t = int(timestep.reshape(-1)[0].item()) if torch.is_tensor(timestep) else int(timestep)
+        if torch.is_tensor(timestep):
+            tv = timestep.reshape(-1)
+            if tv.numel() == 0:
+                raise ValueError("empty timestep tensor")
+            # the reference broadcasts one timestep over the batch (unet.py:361-374); a
+            # per-sample vector would need one embedding per sample, which the
+            # inference loop never passes -- refuse it instead of using tv[0] silently
+            if tv.numel() > 1 and not bool((tv == tv[0]).all()):
+                raise NotImplementedError("per-sample timesteps (distinct values) are not on the inference path")
+            t = int(tv[0].item())
+        else:
+            t = int(timestep)
         ts = torch.tensor([t], dtype=torch.int32, device=sample.device)
         step = torch.zeros(1, dtype=torch.int32, device=sample.device)
         audio, ntok = None, 0

@@ -192,11 +192,13 @@ def main():
         gen_blocks(resnet, attention, motion)
     if want("tiny"):
         gen_unet(unet, TINY_MODEL, "unet_tiny.npz", 31,
-                 [(1, 16, 32, 951, False), (2, 8, 16, 501, True), (1, 1, 32, 1, False)])
+                 [(1, 16, 32, 951, False), (2, 8, 16, 501, True), (1, 1, 32, 1, False),
+                  (1, 16, 64, 951, False), (2, 16, 64, 501, True)])  # configs[4] latent 64^2
     if want("whisper"):
         gen_whisper()
     if want("full") and not a.skip_full:
-        gen_unet(unet, STAGE2_MODEL, "unet_full.npz", 41, [(1, 16, 32, 951, False), (1, 1, 32, 1, False)])
+        gen_unet(unet, STAGE2_MODEL, "unet_full.npz", 41, [(1, 16, 32, 951, False), (1, 1, 32, 1, False),
+                  (2, 16, 32, 501, True)])  # CFG batch (configs[2])
 
 
 if __name__ == "__main__":

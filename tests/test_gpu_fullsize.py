@@ -1,0 +1,111 @@
+"""Parity at the configurations' real sizes (BASELINE.json configs[1], [2], [4]):
+
+  * the full-width SD VAE (block_out_channels 128/256/512/512) encode + decode at
+    256^2 on 4 frames and at 512^2 on 2 frames -- including the mid-block
+    attention at d = 512 over N = 1024 / 4096 tokens -- against the fp32 oracle;
+  * one full-size window (LatentSync-1.5 stage2 UNet + full VAE, 8 frames, 2 DDIM
+    steps, with and without CFG) against oracle.pipeline_window.
+
+Tolerances (bf16 storage, fp32 accumulation, against fp32):
+  * rel-L2 < 3e-2 on VAE moments / decoded pixels / window output (as the other
+    parity tests);
+  * per-pixel, on the uint8 pixels the pipeline emits ((x/2+0.5).clamp(0,1)*255,
+    truncated): max |delta| <= 8 levels and 99.9th percentile <= 3 levels over the
+    generated (mouth) region; outside it the pasted-back original pixels are equal
+    up to 1 level.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+
+SCHED = dict(beta_end=0.012, beta_schedule="scaled_linear", beta_start=0.00085, clip_sample=False,
+             num_train_timesteps=1000, set_alpha_to_one=False, steps_offset=1)
+PIX_MAX, PIX_P999 = 8, 3
+
+
+def _u8(x):
+    return ((x.float() / 2 + 0.5).clamp(0, 1) * 255).to(torch.uint8).to(torch.int32)
+
+
+def _pixel_check(out, ref, region):
+    d = (_u8(out) - _u8(ref)).abs()[region.expand_as(out)].float()
+    mx, p999 = float(d.max()), float(torch.quantile(d[: 1 << 24], 0.999))
+    print(f"per-pixel uint8 |delta|: max {mx:.0f}, p99.9 {p999:.0f}, mean {float(d.mean()):.3f}")
+    assert mx <= PIX_MAX and p999 <= PIX_P999, (mx, p999)
+
+
+@pytest.fixture(scope="module")
+def vae():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from latentsync_amd.vae import AutoencoderKL
+    return AutoencoderKL().init_weights(51).to("cuda")
+
+
+@pytest.mark.parametrize("R,n", [(256, 4), (512, 2)])
+def test_vae_full_width(vae, R, n):
+    from oracle import ref_cpu as O
+    torch.set_num_threads(16)
+    g = torch.Generator().manual_seed(R + n)
+    low = torch.rand((n, 3, R // 16, R // 16), generator=g)
+    x = torch.nn.functional.interpolate(low, size=(R, R), mode="bilinear") * 2 - 1
+    with torch.no_grad():
+        mom = vae.encode(x.cuda()).latent_dist.parameters.float().cpu()
+        mref = O.vae_encode_moments(vae._sd, x)
+        e = rel_err(mom, mref)
+        print("VAE encode moments rel_err", R, e)
+        assert mom.shape == (n, 8, R // 8, R // 8) and e < 3e-2
+        z = torch.randn((n, 4, R // 8, R // 8), generator=g)
+        dec = vae.decode(z.cuda()).sample.float().cpu()
+        dref = O.vae_decode(vae._sd, z)
+    e = rel_err(dec, dref)
+    print("VAE decode rel_err", R, e)
+    assert dec.shape == (n, 3, R, R) and e < 3e-2
+    _pixel_check(dec, dref, torch.ones((1, 1, R, R), dtype=torch.bool))
+
+
+@pytest.fixture(scope="module")
+def unet_full():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from latentsync_amd.config import STAGE2_MODEL
+    from latentsync_amd.unet import UNet3DConditionModel
+    return UNet3DConditionModel(**STAGE2_MODEL).init_weights(41).to("cuda").eval()
+
+
+@pytest.mark.parametrize("guidance", [1.0, 2.0])
+def test_full_size_window(vae, unet_full, guidance):
+    """stage2 UNet + full VAE at 256^2: the per-pixel bound on the regenerated mouth."""
+    from latentsync_amd.pipeline import WindowEngine, load_fixed_mask
+    from latentsync_amd.scheduler import DDIMScheduler
+    from oracle import ref_cpu as O
+    torch.set_num_threads(16)
+    Fr, R, steps = 8, 256, 2
+    h = R // 8
+    unet = unet_full
+    g = torch.Generator().manual_seed(9)
+    low = torch.rand((Fr, 3, R // 16, R // 16), generator=g)
+    faces = (torch.nn.functional.interpolate(low, size=(R, R), mode="bilinear") * 255).round().to(torch.uint8)
+    mask = load_fixed_mask(R)
+    audio = torch.randn((Fr, 50, 384), generator=g)
+    init = torch.randn((1, 4, 1, h, h), generator=g)
+    em, er = torch.randn((Fr, 4, h, h), generator=g), torch.randn((Fr, 4, h, h), generator=g)
+    eng = WindowEngine(unet, vae, DDIMScheduler(**SCHED), Fr, R, steps, guidance)
+    eng.load(faces.cuda(), mask.cuda(), audio.cuda(), init.cuda(), em.cuda(), er.cuda())
+    out = eng.run().float().cpu()
+    with torch.no_grad():
+        ref = O.pipeline_window(unet.state_dict(), dict(unet.config), vae._sd, faces, mask, audio, init, em, er,
+                                num_steps=steps, guidance_scale=guidance)
+    e = rel_err(out, ref)
+    print("full-size window rel_err", guidance, e)
+    assert e < 3e-2
+    mouth = (mask < 1)[None, None]
+    _pixel_check(out, ref, mouth)
+    keep = (mask == 1)[None, None].expand_as(out)
+    assert int((_u8(out) - _u8(ref)).abs()[keep].max()) <= 1
+    # the uint8 frames the engine hands to the gather / writer are the same pixels
+    assert torch.equal(eng.out_u8.cpu().permute(0, 3, 1, 2).to(torch.int32), _u8(out))

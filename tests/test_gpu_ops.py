@@ -152,7 +152,11 @@ def _sdpa(q, k, v, scale=None):
 @pytest.mark.parametrize("n,N,Nk,heads,d", [(4, 256, 256, 8, 40), (2, 64, 64, 8, 80), (2, 16, 16, 8, 160),
                                             (3, 256, 50, 8, 40), (2, 64, 50, 8, 160), (1, 100, 100, 6, 64),
                                             (2, 64, 64, 1, 512), (2, 1024, 1024, 1, 128), (2, 64, 64, 8, 4),
-                                            (2, 1000, 777, 8, 40), (2, 200, 130, 8, 80)])
+                                            (2, 1000, 777, 8, 40), (2, 200, 130, 8, 80),
+                                            # configs[4] (latent 64^2): spatial N = 4096 / 1024, audio cross
+                                            (1, 4096, 4096, 8, 40), (2, 1024, 1024, 8, 80), (1, 4096, 50, 8, 40),
+                                            # SD-VAE mid attention at 256^2: 1 head, d = 512, N = 1024
+                                            (2, 1024, 1024, 1, 512)])
 def test_attention_spatial(gpu, n, N, Nk, heads, d):
     C = heads * d
     q = bf(rnd(n, N, C, seed=50))

@@ -42,7 +42,7 @@ def test_window_matches_oracle(gpu, guidance, graphs, monkeypatch):
     print("window rel_err", guidance, graphs, e)
     assert e < 3e-2
     # outside the mouth the original pixels are pasted back exactly (up to bf16 of the prep)
-    keep = mask.bool()[None, None].expand_as(ref)
+    keep = (mask == 1)[None, None].expand_as(ref)
     assert (out[keep] - ref[keep]).abs().max() < 1e-2
 
 
@@ -115,3 +115,30 @@ def test_run_windows_batches_match_oracle(gpu, monkeypatch):
         e = rel_err(out[sl].cpu(), ref)
         print("run_windows window", w, e)
         assert e < 3e-2
+
+
+def test_window_configs4_shape(gpu, monkeypatch):
+    """configs[4]'s shapes: 512^2 faces, 64^2 latent (spatial attention N = 4096 at the
+    top UNet level), the 512^2 mask from the LANCZOS4 resize (fractional edge values
+    in both the pixel mask and the nearest-interpolated latent mask)."""
+    Fr, Rr, steps = 8, 512, 2
+    h = Rr // 8
+    unet = UNet3DConditionModel(**TINY_MODEL).init_weights(12).to("cuda").eval()
+    vae = AutoencoderKL(block_out_channels=(32, 64, 64, 64)).init_weights(13).to("cuda")
+    monkeypatch.setitem(R.VAE_CFG, "block_out_channels", (32, 64, 64, 64))
+    g = torch.Generator().manual_seed(14)
+    low = torch.rand((Fr, 3, Rr // 32, Rr // 32), generator=g)
+    faces = (torch.nn.functional.interpolate(low, size=(Rr, Rr), mode="bilinear") * 255).round().to(torch.uint8)
+    mask = load_fixed_mask(Rr)
+    assert ((mask > 0) & (mask < 1)).any()
+    audio = torch.randn((Fr, 50, 384), generator=g)
+    init = torch.randn((1, 4, 1, h, h), generator=g)
+    em, er = torch.randn((Fr, 4, h, h), generator=g), torch.randn((Fr, 4, h, h), generator=g)
+    eng = WindowEngine(unet, vae, DDIMScheduler(**SCHED), Fr, Rr, steps, 1.0)
+    eng.load(faces.cuda(), mask.cuda(), audio.cuda(), init.cuda(), em.cuda(), er.cuda())
+    out = eng.run().cpu()
+    ref = R.pipeline_window(unet.state_dict(), dict(unet.config), vae._sd, faces, mask, audio, init, em, er,
+                            num_steps=steps, guidance_scale=1.0)
+    e = rel_err(out, ref)
+    print("configs[4]-shape window rel_err", e)
+    assert e < 3e-2
