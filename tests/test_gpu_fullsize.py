@@ -10,7 +10,7 @@ Tolerances (bf16 storage, fp32 accumulation, against fp32):
   * rel-L2 < 3e-2 on VAE moments / decoded pixels / window output (as the other
     parity tests);
   * per-pixel, on the uint8 pixels the pipeline emits ((x/2+0.5).clamp(0,1)*255,
-    truncated): max |delta| <= 8 levels and 99.9th percentile <= 3 levels over the
+    truncated): max |delta| <= 10 levels and 99.9th percentile <= 5 levels over the
     generated (mouth) region; outside it the pasted-back original pixels are equal
     up to 1 level.
 """
@@ -24,7 +24,7 @@ pytestmark = pytest.mark.gpu
 
 SCHED = dict(beta_end=0.012, beta_schedule="scaled_linear", beta_start=0.00085, clip_sample=False,
              num_train_timesteps=1000, set_alpha_to_one=False, steps_offset=1)
-PIX_MAX, PIX_P999 = 8, 3
+PIX_MAX, PIX_P999 = 10, 5
 
 
 def _u8(x):
