@@ -10,6 +10,14 @@
 // O^T = V^T P^T, with no LDS round trip: the MFMA's k index is permuted
 // identically on both operands (keys 32c+4h+j and 32c+16+4h+j for lane group h),
 // and V^T comes from the row-major V tile through ds_read_b64_tr_b16.
+//
+// Kernels (dispatch in ls_attention):
+//   attn_seq_kernel  short sequences (the temporal attention over a window's frames)
+//   attn5_kernel     d = 40 self attention: DMA-fed K/V planes, 64 queries per wave
+//   attn3_kernel     other long sequences (register-staged K/V tiles)
+//   attn_kernel      everything else (nk <= 32, d > 160: the VAE mid attention)
+// attn3/attn5 share the softmax scheme: Q pre-scaled to log2 units, the running max
+// subtracted by the MFMA's C operand, lazy rescaling, bf16 P.
 #include <type_traits>
 
 #include "ls_common.h"
@@ -175,22 +183,34 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
   }
 }
 
-// Long-sequence variant (nk > 32): every wave owns 32 queries (two Q fragments
-// share each K/V fragment read), 64-key tiles double-buffered in LDS with the
-// next tile's global loads issued into registers before the current tile's
-// MFMAs (one barrier per tile), QK^T over KC 32-wide d chunks but PV over only
-// ND = ceil(D/16) output fragments (d = 40 pays 48, not 64), and the softmax
-// exponent formed with one FMA (s * scale*log2e - m).
-typedef float f2v __attribute__((ext_vector_type(2)));
-
-template <int KC, int ND>
-__global__ void __launch_bounds__(256, KC >= 5 ? 1 : 2) attn2_kernel(AttnArgs a) {
+// attn3: long-sequence flash attention (nk > 32).  Every wave owns 32 queries (two Q
+// fragments share each K/V fragment read), 64-key tiles double-buffered in LDS with
+// the next tile's global loads issued into registers before the current tile's
+// MFMAs (one barrier per tile), QK^T over KC 32-wide d chunks, PV over ND = ceil(D/16)
+// output fragments (d = 40 pays 48, not 64).  The softmax costs ~2 VALU instructions
+// per score (round 1's kernel spent ~215 VALU instructions per 64-key tile at d = 40
+// against 28 MFMAs):
+//   * Q is pre-scaled by scale*log2(e) once (bf16), so a score leaves the MFMA in
+//     log2 units;
+//   * the running max m is SUBTRACTED BY THE MFMA: the first QK^T step of every
+//     fragment accumulates onto C = -m (a 4-register splat), so p = exp2(s) with no
+//     FMA per score;
+//   * lazy rescaling: m is only moved (and O, l rescaled) when a tile's max exceeds
+//     it by more than TAU = 10 (p <= 2^10 is exact enough in bf16/fp32); the check
+//     is one wave-uniform ballot per tile, the rescale path is rare after tile 0;
+//   * DSUM = D with D % 16 != 0 (d = 40): the row sum l comes out of the PV MFMA --
+//     V's padding column D is set to 1.0 once, so O^T row D accumulates sum_k p_k
+//     (of the same bf16 p the numerator uses) and the 16 adds per score row go away.
+template <int KC, int ND, int DSUM>
+__global__ void __launch_bounds__(256, KC >= 5 ? 1 : 2) attn3_kernel(AttnArgs a) {
   constexpr int DP = KC * 32;
   constexpr int KT = 64;
   constexpr int PITCH = DP + 8;
-  constexpr int TILE = KT * PITCH;          // elements per K (or V) tile
-  constexpr int CPR = ND * 2;               // max 16-B chunks per row actually loaded (D <= 16 ND)
-  constexpr int LPT = (KT * CPR + 255) / 256;  // chunks per thread per operand
+  constexpr int TILE = KT * PITCH;
+  constexpr int CPR = ND * 2;
+  constexpr int LPT = (KT * CPR + 255) / 256;
+  constexpr float TAU = 10.f;
+  static_assert(DSUM == 0 || (DSUM % 8 == 0 && DSUM < 16 * ND), "sum column must be a padding column");
   extern __shared__ __attribute__((aligned(16))) u16 sm[];  // [2][K, V]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -203,14 +223,21 @@ __global__ void __launch_bounds__(256, KC >= 5 ? 1 : 2) attn2_kernel(AttnArgs a)
   u16* ob = a.o + b1 * a.o_sb1 + b2 * a.o_sb2 + (long)h * a.o_sh;
   const int q0 = (blockIdx.x * 4 + wid) * 32;
   const int lq = lane & 15, lg = lane >> 4;
-  const int cpr = (a.D + 7) >> 3;           // chunks per row present in memory
+  const int cpr = (a.D + 7) >> 3;
 
-  // zero the d padding of both K buffers once (QK^T reads d up to DP)
+  // K d-padding zeroed in both buffers; with DSUM, V[:, DSUM] = 1 and the rest of the
+  // padding 0 (the per-tile stores never touch chunks >= cpr)
   for (int i = tid; i < 2 * KT; i += 256) {
-    u16* row = sm + (i / KT) * 2 * TILE + (i % KT) * PITCH;
-    for (int c = cpr * 8; c < DP; c += 8) *(uint4*)(row + c) = make_uint4(0, 0, 0, 0);
+    u16* krow = sm + (i / KT) * 2 * TILE + (i % KT) * PITCH;
+    for (int c = cpr * 8; c < DP; c += 8) *(uint4*)(krow + c) = make_uint4(0, 0, 0, 0);
+    if (DSUM) {
+      u16* vrow = krow + TILE;
+      for (int c = cpr * 8; c < 16 * ND; c += 8)
+        *(uint4*)(vrow + c) = make_uint4(c == DSUM ? 0x3F80u : 0u, 0, 0, 0);
+    }
   }
 
+  const float c2 = a.scale_log2;
   bf16x8 qf[2][KC];
 #pragma unroll
   for (int g = 0; g < 2; ++g)
@@ -220,7 +247,11 @@ __global__ void __launch_bounds__(256, KC >= 5 ? 1 : 2) attn2_kernel(AttnArgs a)
       const int q = q0 + g * 16 + lq;
       uint4 v = make_uint4(0, 0, 0, 0);
       if (q < a.nq && d < a.D) v = *(const uint4*)(qb + (long)q * a.q_si + d);
-      qf[g][kc] = __builtin_bit_cast(bf16x8, v);
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] *= c2;
+      qf[g][kc] = __builtin_bit_cast(bf16x8, pack8(f));
     }
 
   uint4 kr[LPT], vr[LPT];
@@ -256,32 +287,29 @@ __global__ void __launch_bounds__(256, KC >= 5 ? 1 : 2) attn2_kernel(AttnArgs a)
   for (int g = 0; g < 2; ++g)
 #pragma unroll
     for (int i = 0; i < ND; ++i) oacc[g][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
-  const float c2 = a.scale_log2;
+  float m[2] = {0.f, 0.f}, l[2] = {0.f, 0.f};
+  f32x4 negm[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
 
   gload(0);
-  __syncthreads();  // padding zeroed
+  __syncthreads();  // padding written
   lstore(0);
   const int ntile = (a.nk + KT - 1) / KT;
-  // one 64-key tile; PARTIAL (the last tile when nk % 64 != 0) masks keys >= nk
   auto tile = [&](int t, auto partial_tag) {
     constexpr bool PARTIAL = decltype(partial_tag)::value;
     const int t0 = t * KT;
-    __syncthreads();  // tile t visible; buffer t^1 free
+    __syncthreads();
     if (t + 1 < ntile) gload(t0 + KT);
     const u16* Ks = sm + (t & 1) * 2 * TILE;
     const u16* Vs = Ks + TILE;
-    // S^T = K Q^T for both query fragments
+    // S^T - m = K Q^T + (-m): scores relative to the running max, log2 units
     f32x4 s[2][4];
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
-      s[0][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      s[1][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
         const bf16x8 kf = __builtin_bit_cast(bf16x8, *(const uint4*)(Ks + (16 * f + lq) * PITCH + kc * 32 + lg * 8));
-        s[0][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[0][kc], s[0][f], 0, 0, 0);
-        s[1][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[1][kc], s[1][f], 0, 0, 0);
+        s[0][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[0][kc], kc == 0 ? negm[0] : s[0][f], 0, 0, 0);
+        s[1][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[1][kc], kc == 0 ? negm[1] : s[1][f], 0, 0, 0);
       }
     }
 #pragma unroll
@@ -293,7 +321,6 @@ __global__ void __launch_bounds__(256, KC >= 5 ? 1 : 2) attn2_kernel(AttnArgs a)
           for (int r = 0; r < 4; ++r)
             if (t0 + 16 * f + 4 * lg + r >= a.nk) s[g][f][r] = -INFINITY;
       }
-      // running max: IEEE maximum (v_maximum3_f32), no NaN-canonicalising self-max per input
       float mt = __builtin_elementwise_maximum(__builtin_elementwise_maximum(s[g][0][0], s[g][0][1]),
                                                __builtin_elementwise_maximum(s[g][0][2], s[g][0][3]));
 #pragma unroll
@@ -301,23 +328,31 @@ __global__ void __launch_bounds__(256, KC >= 5 ? 1 : 2) attn2_kernel(AttnArgs a)
         mt = __builtin_elementwise_maximum(
             mt, __builtin_elementwise_maximum(__builtin_elementwise_maximum(s[g][f][0], s[g][f][1]),
                                               __builtin_elementwise_maximum(s[g][f][2], s[g][f][3])));
-      mt = __builtin_elementwise_maximum(mt, __shfl_xor(mt, 16, 64));
-      mt = __builtin_elementwise_maximum(mt, __shfl_xor(mt, 32, 64));
-      const float mn = __builtin_elementwise_maximum(m[g], mt * c2);
-      const float alpha = fast_exp2(m[g] - mn);
-      m[g] = mn;
-      float ps = 0.f;
+      mt = xor16_32_max(mt);
+      // move the reference max only when needed (always on the first tile, which
+      // starts from m = 0 with nothing accumulated)
+      const bool need = t == 0 || mt > TAU;
+      if (__builtin_amdgcn_ballot_w64(need)) {
+        const float dlt = need ? mt : 0.f;
+        const float alpha = t == 0 ? 0.f : fast_exp2(-dlt);
+        m[g] += dlt;
+        negm[g] = (f32x4){-m[g], -m[g], -m[g], -m[g]};
+#pragma unroll
+        for (int f = 0; f < 4; ++f) s[g][f] -= dlt;
+#pragma unroll
+        for (int i = 0; i < ND; ++i) oacc[g][i] *= alpha;
+        l[g] *= alpha;
+      }
 #pragma unroll
       for (int f = 0; f < 4; ++f)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = fast_exp2(fmaf(s[g][f][r], c2, -mn));
-          s[g][f][r] = p;
-          ps += p;
-        }
-      l[g] = fmaf(l[g], alpha, ps);
+        for (int r = 0; r < 4; ++r) s[g][f][r] = fast_exp2(s[g][f][r]);
+      if (!DSUM) {
+        float ps = 0.f;
 #pragma unroll
-      for (int i = 0; i < ND; ++i) oacc[g][i] *= alpha;
+        for (int f = 0; f < 4; ++f) ps += (s[g][f][0] + s[g][f][1]) + (s[g][f][2] + s[g][f][3]);
+        l[g] += ps;
+      }
     }
     // O^T += V^T P^T over 32-key chunks
 #pragma unroll
@@ -350,9 +385,14 @@ __global__ void __launch_bounds__(256, KC >= 5 ? 1 : 2) attn2_kernel(AttnArgs a)
   if (nfull < ntile) tile(nfull, std::true_type{});
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
-    float lt = l[g];
-    lt += __shfl_xor(lt, 16, 64);
-    lt += __shfl_xor(lt, 32, 64);
+    float lt;
+    if (DSUM) {
+      // O^T row DSUM (fragment DSUM/16, lane group (DSUM%16)/4, register DSUM%4) holds l
+      constexpr int NDL = DSUM / 16, LGL = (DSUM % 16) / 4, RL = DSUM % 4;
+      lt = __shfl(oacc[g][NDL][RL], LGL * 16 + lq, 64);
+    } else {
+      lt = xor16_32_sum(l[g]);
+    }
     const float inv = 1.f / lt;
     const int q = q0 + g * 16 + lq;
     if (q < a.nq) {
@@ -375,19 +415,323 @@ __global__ void __launch_bounds__(256, KC >= 5 ? 1 : 2) attn2_kernel(AttnArgs a)
   }
 }
 
-template <int KC, int ND>
-static int launch_attn2(const AttnArgs& a, int batch, int heads, hipStream_t s) {
+// attn5: attn3's arithmetic with the K/V tiles moved by buffer_load ... lds DMA.
+// attn3's register-staged tile copy cost ~60 VALU per tile (64-bit address math,
+// exec-masked tails, ds_writes) beside the softmax, and its 144-B-pitch image had
+// 2-way bank conflicts.  Here every K/V tile is stored "chunk-plane major": plane c
+// holds the 16-B chunk c (head dims 8c .. 8c+7) of the tile's 64 keys, one
+// wave-instruction of DMA per plane (lane = key).  The per-lane byte offset
+// (key * row stride + 16 c) is fixed for the whole kernel and the tile advances
+// through the uniform soffset, so a tile costs no VALU at all; keys >= nk fall
+// outside the buffer descriptor's range and load zeros.  Planes past the head dim
+// are written once: K's are zero, V's plane D/8 holds the 1.0 sum column (DSUM).
+// K fragment reads (ds_read_b128, 16 keys x one plane per 16-lane group) are
+// conflict-free; V planes are stored with a rotation of 8 keys per plane so the
+// transposed PV reads (ds_read_b64_tr_b16 over two adjacent planes) are too.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+__device__ void ls_raw_buffer_load_lds(i32x4 rsrc, __attribute__((address_space(3))) void* lds, int size, int voffset,
+                                       int soffset, int offset, int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
+
+__device__ __forceinline__ i32x4 buffer_rsrc(const void* base, uint32_t bytes) {
+  const unsigned long long b = (unsigned long long)base;
+  i32x4 r;
+  r[0] = (int)(uint32_t)b;
+  r[1] = (int)(uint32_t)(b >> 32);  // stride 0
+  r[2] = (int)bytes;                // num_records (bytes): loads at or past it return 0
+  r[3] = 0x00020000;                // gfx9 raw-buffer dword 3
+  return r;
+}
+
+template <int N>
+__device__ __forceinline__ void attn_wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (an immediate per case)
+__device__ __forceinline__ void attn_wait_vm_dyn(int n) {
+  switch (n) {
+    case 0: attn_wait_vm<0>(); break;
+    case 1: attn_wait_vm<1>(); break;
+    case 2: attn_wait_vm<2>(); break;
+    case 3: attn_wait_vm<3>(); break;
+    case 4: attn_wait_vm<4>(); break;
+    case 5: attn_wait_vm<5>(); break;
+    case 6: attn_wait_vm<6>(); break;
+    case 7: attn_wait_vm<7>(); break;
+    case 8: attn_wait_vm<8>(); break;
+    case 9: attn_wait_vm<9>(); break;
+    case 10: attn_wait_vm<10>(); break;
+    default: attn_wait_vm<0>(); break;
+  }
+}
+
+// XCD-aware order (blocks b and b + 8 share an XCD under round-robin dispatch): every
+// XCD gets a contiguous range of logical blocks, so the query blocks of one (batch,
+// head) -- which read the same K/V tiles -- run together on one L2.
+__device__ __forceinline__ int attn_xcd_remap(int b, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = b % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+}
+
+template <int KC, int ND, int DSUM, int QG>
+__global__ void __launch_bounds__(256, 2) attn5_kernel(AttnArgs a, int nqb, int heads) {
+  constexpr int KT = 64;
+  constexpr int NST = 3;                   // LDS ring: tile t computed while t+1, t+2 land
+  constexpr int KPL = KC * 4;              // K planes (32-wide d chunks x 4)
+  constexpr int VPL = ND * 2;              // V planes (16-wide d fragments x 2)
+  constexpr int PLANE = KT * 8;            // elements per plane (64 keys x 8)
+  constexpr int STAGE = (KPL + VPL) * PLANE;
+  constexpr int QW = 16 * QG;              // queries per wave
+  constexpr float TAU = 10.f;
+  static_assert(DSUM == 0 || (DSUM % 8 == 0 && DSUM < 16 * ND), "sum column must be a padding column");
+  extern __shared__ __attribute__((aligned(16))) u16 sm[];  // [NST][K planes, V planes] + dummy plane
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lb = attn_xcd_remap(blockIdx.x, gridDim.x);
+  const int qblk = lb % nqb, pair = lb / nqb;
+  const int h = pair % heads;
+  const int b = pair / heads;
+  const long b1 = b / a.z2, b2 = b - b1 * a.z2;
+  const u16* qb = a.q + b1 * a.q_sb1 + b2 * a.q_sb2 + (long)h * a.q_sh;
+  const u16* kb = a.k + b1 * a.k_sb1 + b2 * a.k_sb2 + (long)h * a.k_sh;
+  const u16* vb = a.v + b1 * a.v_sb1 + b2 * a.v_sb2 + (long)h * a.v_sh;
+  u16* ob = a.o + b1 * a.o_sb1 + b2 * a.o_sb2 + (long)h * a.o_sh;
+  const int q0 = (qblk * 4 + wid) * QW;
+  const int lq = lane & 15, lg = lane >> 4;
+  const int cpr = (a.D + 7) >> 3;           // planes that carry data
+
+  // constant planes of every stage: K's zero, V's sum column / zero
+  for (int i = tid; i < NST * (KPL + VPL) * KT; i += 256) {
+    const int r = i % KT, c = (i / KT) % (KPL + VPL), st = i / (KT * (KPL + VPL));
+    const bool isv = c >= KPL;
+    const int cc = isv ? c - KPL : c;
+    if (cc >= cpr)
+      *(uint4*)(sm + st * STAGE + c * PLANE + r * 8) = make_uint4(isv && DSUM && cc * 8 == DSUM ? 0x3F80u : 0u, 0, 0, 0);
+  }
+
+  const float c2 = a.scale_log2;
+  bf16x8 qf[QG][KC];
+#pragma unroll
+  for (int g = 0; g < QG; ++g)
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      const int d = kc * 32 + lg * 8;
+      const int q = q0 + g * 16 + lq;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (q < a.nq && d < a.D) v = *(const uint4*)(qb + (long)q * a.q_si + d);
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] *= c2;
+      qf[g][kc] = __builtin_bit_cast(bf16x8, pack8(f));
+    }
+
+  // DMA: the 2 cpr plane loads of a tile are dealt round-robin to the 4 waves, padded
+  // to the same count per wave (extra loads re-fetch plane 0 of K into a dummy plane)
+  // so every wave's wait is one constant vmcnt
+  const uint32_t kst = (uint32_t)a.k_si * 2, vst = (uint32_t)a.v_si * 2;
+  const i32x4 krs = buffer_rsrc(kb, (uint32_t)(a.nk - 1) * kst + cpr * 16);
+  const i32x4 vrs = buffer_rsrc(vb, (uint32_t)(a.nk - 1) * vst + cpr * 16);
+  constexpr int NDMA = (2 * ((KC * 32 < ND * 16 ? KC * 32 : ND * 16) / 8) + 3) / 4;  // per wave, upper bound
+  u16* dummy = sm + NST * STAGE;
+  auto issue = [&](int t) {
+    const int t0 = t * KT;
+    u16* st = sm + (t % NST) * STAGE;
+#pragma unroll
+    for (int u = 0; u < NDMA; ++u) {
+      const int j = wid + 4 * u;  // wave-uniform
+      const bool live = j < 2 * cpr;
+      const bool isv = live && j >= cpr;
+      const int c = !live ? 0 : (isv ? j - cpr : j);
+      const int key = isv ? ((lane - 8 * c) & 63) : lane;
+      u16* dst = live ? st + ((isv ? KPL : 0) + c) * PLANE : dummy;
+      ls_raw_buffer_load_lds(isv ? vrs : krs, (__attribute__((address_space(3))) void*)dst, 16,
+                             key * (int)(isv ? vst : kst) + c * 16, t0 * (int)(isv ? vst : kst), 0, 0);
+    }
+  };
+
+  f32x4 oacc[QG][ND];
+#pragma unroll
+  for (int g = 0; g < QG; ++g)
+#pragma unroll
+    for (int i = 0; i < ND; ++i) oacc[g][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m[QG], l[QG];
+  f32x4 negm[QG];
+#pragma unroll
+  for (int g = 0; g < QG; ++g) {
+    m[g] = 0.f;
+    l[g] = 0.f;
+    negm[g] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+
+  const int ntile = (a.nk + KT - 1) / KT;
+  issue(0);
+  if (ntile > 1) issue(1);
+  auto tile = [&](int t, auto partial_tag) {
+    constexpr bool PARTIAL = decltype(partial_tag)::value;
+    const int t0 = t * KT;
+    if (t + 1 < ntile) attn_wait_vm<NDMA>();  // this wave's DMA of tile t landed (t+1's may fly)
+    else attn_wait_vm<0>();
+    __syncthreads();                          // everyone's; slot (t+2) % 3 free
+    if (t + 2 < ntile) issue(t + 2);
+    const u16* Ks = sm + (t % NST) * STAGE;
+    const u16* Vs = Ks + KPL * PLANE;
+    f32x4 s[QG][4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        const bf16x8 kf = __builtin_bit_cast(bf16x8, *(const uint4*)(Ks + (kc * 4 + lg) * PLANE + (16 * f + lq) * 8));
+#pragma unroll
+        for (int g = 0; g < QG; ++g)
+          s[g][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[g][kc], kc == 0 ? negm[g] : s[g][f], 0, 0, 0);
+      }
+    }
+    float mt[QG];
+    bool need_any = t == 0;
+#pragma unroll
+    for (int g = 0; g < QG; ++g) {
+      if (PARTIAL) {
+#pragma unroll
+        for (int f = 0; f < 4; ++f)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (t0 + 16 * f + 4 * lg + r >= a.nk) s[g][f][r] = -INFINITY;
+      }
+      float x = __builtin_elementwise_maximum(__builtin_elementwise_maximum(s[g][0][0], s[g][0][1]),
+                                              __builtin_elementwise_maximum(s[g][0][2], s[g][0][3]));
+#pragma unroll
+      for (int f = 1; f < 4; ++f)
+        x = __builtin_elementwise_maximum(
+            x, __builtin_elementwise_maximum(__builtin_elementwise_maximum(s[g][f][0], s[g][f][1]),
+                                             __builtin_elementwise_maximum(s[g][f][2], s[g][f][3])));
+      mt[g] = xor16_32_max(x);
+      need_any |= mt[g] > TAU;
+    }
+    // one wave-uniform check per tile: move the reference max of the rows whose tile
+    // max exceeds it by TAU (every row on the first tile)
+    if (__builtin_amdgcn_ballot_w64(need_any)) {
+#pragma unroll
+      for (int g = 0; g < QG; ++g) {
+        const bool need = t == 0 || mt[g] > TAU;
+        const float dlt = need ? mt[g] : 0.f;
+        const float alpha = t == 0 ? 0.f : fast_exp2(-dlt);
+        m[g] += dlt;
+        negm[g] = (f32x4){-m[g], -m[g], -m[g], -m[g]};
+#pragma unroll
+        for (int f = 0; f < 4; ++f) s[g][f] -= dlt;
+#pragma unroll
+        for (int i = 0; i < ND; ++i) oacc[g][i] *= alpha;
+        l[g] *= alpha;
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < QG; ++g) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[g][f][r] = fast_exp2(s[g][f][r]);
+      if (!DSUM) {
+        float ps = 0.f;
+#pragma unroll
+        for (int f = 0; f < 4; ++f) ps += (s[g][f][0] + s[g][f][1]) + (s[g][f][2] + s[g][f][3]);
+        l[g] += ps;
+      }
+    }
+    // O^T += V^T P^T over 32-key chunks; a lane reads 4 dims of one key from plane
+    // 2 nd + pp/2 (rows rotated by 8 keys per plane)
+    const int qq = lq >> 2, pp = lq & 3;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      bf16x8 pb[QG];
+#pragma unroll
+      for (int g = 0; g < QG; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pb[g][r] = (__bf16)s[g][2 * c][r];
+          pb[g][4 + r] = (__bf16)s[g][2 * c + 1][r];
+        }
+      const int key = 32 * c + 4 * lg + qq;
+#pragma unroll
+      for (int nd = 0; nd < ND; ++nd) {
+        const int pl = 2 * nd + (pp >> 1);
+        const u16* plane = Vs + pl * PLANE + (pp & 1) * 4;
+        const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4i16*)(plane + ((key + 8 * pl) & 63) * 8));
+        const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4i16*)(plane + ((key + 16 + 8 * pl) & 63) * 8));
+        const short __attribute__((ext_vector_type(8))) av = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const bf16x8 vf = __builtin_bit_cast(bf16x8, av);
+#pragma unroll
+        for (int g = 0; g < QG; ++g)
+          oacc[g][nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[g], oacc[g][nd], 0, 0, 0);
+      }
+    }
+  };
+  const int nfull = a.nk / KT;
+  for (int t = 0; t < nfull; ++t) tile(t, std::false_type{});
+  if (nfull < ntile) tile(nfull, std::true_type{});
+#pragma unroll
+  for (int g = 0; g < QG; ++g) {
+    float lt;
+    if (DSUM) {
+      constexpr int NDL = DSUM / 16, LGL = (DSUM % 16) / 4, RL = DSUM % 4;
+      lt = __shfl(oacc[g][NDL][RL], LGL * 16 + lq, 64);
+    } else {
+      lt = xor16_32_sum(l[g]);
+    }
+    const float inv = 1.f / lt;
+    const int q = q0 + g * 16 + lq;
+    if (q < a.nq) {
+      u16* orow = ob + (long)q * a.o_si;
+#pragma unroll
+      for (int nd = 0; nd < ND; ++nd) {
+        const int d = nd * 16 + 4 * lg;
+        if (d + 3 < a.D) {
+          uint2 w;
+          w.x = (uint32_t)f2bf(oacc[g][nd][0] * inv) | ((uint32_t)f2bf(oacc[g][nd][1] * inv) << 16);
+          w.y = (uint32_t)f2bf(oacc[g][nd][2] * inv) | ((uint32_t)f2bf(oacc[g][nd][3] * inv) << 16);
+          *(uint2*)(orow + d) = w;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (d + r < a.D) orow[d + r] = f2bf(oacc[g][nd][r] * inv);
+        }
+      }
+    }
+  }
+}
+
+template <int KC, int ND, int DSUM, int QG = 2>
+static int launch_attn5(const AttnArgs& a, int batch, int heads, hipStream_t s) {
+  const int nqb = cdiv(a.nq, 4 * 16 * QG);
+  const long nblk = (long)nqb * heads * batch;
+  if (nblk > 0x7fffffff) return fail(LS_ERR_INVALID, "ls_attention: grid too large");
+  const size_t shm = (3 * (size_t)(KC * 4 + ND * 2) + 1) * 64 * 8 * sizeof(u16);
+  if (shm > 64 * 1024) {
+    static bool attr_set = false;
+    if (!attr_set) {
+      hipFuncSetAttribute((const void*)attn5_kernel<KC, ND, DSUM, QG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)shm);
+      attr_set = true;
+    }
+  }
+  attn5_kernel<KC, ND, DSUM, QG><<<(int)nblk, 256, shm, s>>>(a, nqb, heads);
+  return check_launch("attn5_kernel");
+}
+
+template <int KC, int ND, int DSUM>
+static int launch_attn3(const AttnArgs& a, int batch, int heads, hipStream_t s) {
   const dim3 grid(cdiv(a.nq, 128), heads, batch);
   const size_t shm = 2 * 2 * (size_t)64 * (KC * 32 + 8) * sizeof(u16);
   if (shm > 64 * 1024) {
     static bool attr_set = false;
     if (!attr_set) {
-      hipFuncSetAttribute((const void*)attn2_kernel<KC, ND>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+      hipFuncSetAttribute((const void*)attn3_kernel<KC, ND, DSUM>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)shm);
       attr_set = true;
     }
   }
-  attn2_kernel<KC, ND><<<grid, 256, shm, s>>>(a);
-  return check_launch("attn2_kernel");
+  attn3_kernel<KC, ND, DSUM><<<grid, 256, shm, s>>>(a);
+  return check_launch("attn3_kernel");
 }
 
 template <int DP, int NKF>
@@ -540,6 +884,7 @@ static int launch_seq(const AttnArgs& a, int batch, int heads, hipStream_t s) {
 using namespace ls;
 
 static bool g_attn_v1 = getenv("LS_ATTN_V1") != nullptr;  // A/B switch: force the 16-query kernel
+static bool g_attn_v3 = getenv("LS_ATTN_V3") != nullptr;  // A/B switch: attn3 for d = 40 too
 
 extern "C" int ls_attention(const ls_attn_desc* d, void* stream) {
   if (!d || !d->q || !d->k || !d->v || !d->o) return fail(LS_ERR_INVALID, "ls_attention: null pointer");
@@ -576,15 +921,20 @@ extern "C" int ls_attention(const ls_attn_desc* d, void* stream) {
     }
   }
   if (!small && D % 8 == 0 && D <= 160 && !g_attn_v1) {
-    // ND = ceil(D / 16) output fragments, KC = ceil(D / 32) contraction chunks
+    // d = 40 self attention (the UNet's 32x32 / 64x64 levels): the DMA-fed kernel, 64
+    // queries per wave, row sums from the PV MFMA; short key sets (the 50 audio tokens)
+    // and other head dims: attn3 (register-staged tiles)
+    if (D == 40 && !g_attn_v3 && d->nk > 128 && ((long)(d->nk - 1) * std::max(d->k_si, d->v_si) + D) * 2 < (1L << 31))
+      return launch_attn5<2, 3, 40, 4>(a, d->batch, d->heads, s);
+    if (D == 40) return launch_attn3<2, 3, 40>(a, d->batch, d->heads, s);
     switch ((D + 15) / 16) {
-      case 1: case 2: return launch_attn2<1, 2>(a, d->batch, d->heads, s);
-      case 3: return launch_attn2<2, 3>(a, d->batch, d->heads, s);
-      case 4: return launch_attn2<2, 4>(a, d->batch, d->heads, s);
-      case 5: return launch_attn2<3, 5>(a, d->batch, d->heads, s);
-      case 6: return launch_attn2<3, 6>(a, d->batch, d->heads, s);
-      case 7: case 8: return launch_attn2<4, 8>(a, d->batch, d->heads, s);
-      default: return launch_attn2<5, 10>(a, d->batch, d->heads, s);
+      case 1: case 2: return launch_attn3<1, 2, 0>(a, d->batch, d->heads, s);
+      case 3: return launch_attn3<2, 3, 0>(a, d->batch, d->heads, s);
+      case 4: return launch_attn3<2, 4, 0>(a, d->batch, d->heads, s);
+      case 5: return launch_attn3<3, 5, 0>(a, d->batch, d->heads, s);
+      case 6: return launch_attn3<3, 6, 0>(a, d->batch, d->heads, s);
+      case 7: case 8: return launch_attn3<4, 8, 0>(a, d->batch, d->heads, s);
+      default: return launch_attn3<5, 10, 0>(a, d->batch, d->heads, s);
     }
   }
 #define LS_ATTN(DPV)                                                              \

@@ -74,6 +74,27 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// max / sum over the 4 lanes {L, L^16, L^32, L^48} (the lane groups of a 16x16 MFMA
+// accumulator column) with gfx950's cross-row swaps: VALU only, no LDS round trip
+// (a ds_bpermute per step costs a dependent LDS latency).
+__device__ __forceinline__ float xor16_32_max(float v) {
+  const uint32_t u = __float_as_uint(v);
+  const auto a = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  v = __builtin_elementwise_maximum(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const uint32_t w = __float_as_uint(v);
+  const auto b = __builtin_amdgcn_permlane16_swap(w, w, false, false);
+  return __builtin_elementwise_maximum(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
+__device__ __forceinline__ float xor16_32_sum(float v) {
+  const uint32_t u = __float_as_uint(v);
+  const auto a = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const uint32_t w = __float_as_uint(v);
+  const auto b = __builtin_amdgcn_permlane16_swap(w, w, false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 }  // namespace ls
