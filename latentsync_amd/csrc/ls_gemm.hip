@@ -1437,29 +1437,40 @@ static int g_force_tile = 0, g_force_split = 0, g_ablate = 0, g_bk = 64;
 
 struct TileCfg { int bm, bn, split; };
 
-// Tile + split-K choice by a small cost model: time ~ max(1, blocks / CUs) x
-// per-block MFMA work / relative efficiency of the tile, + split-K slab traffic.
-static TileCfg pick_tile(long M, int N, int ktiles, bool allow_split, bool big_ok) {
-  struct Cand { int bm, bn; double eff; };
-  // eff = relative MFMA throughput of the tile (measured, scripts/gemm_bench.py)
-  const Cand cands[] = {{128, 128, 1.0}, {128, 160, 1.2}, {128, 64, 0.72}, {64, 64, 0.42}, {128, 32, 0.36},
-                        {256, 256, 1.35}};
+// Tile + split-K choice by a small cost model.  A CU runs up to R blocks of a tile
+// at once (LDS-limited: 2 for the 4-wave 128-row tiles, 1 for the 8-wave 256x256);
+// the grid takes ceil(blocks / CUs) block-durations per CU, and a 4-wave tile alone
+// on a CU runs at ~0.75 of its throughput with a second block beside it (measured,
+// scripts/splitk_sweep.py: 128x160 at 256 blocks 685 TF/s, at 512 blocks 838).
+// eff = relative MFMA throughput of the tile; split-K adds its fp32 slab write + read
+// (~1.5 MAC-units per slab element, calibrated on the 4x4-level convs and FF2).
+static TileCfg pick_tile(long M, int N, int ktiles, bool allow_split, bool big_ok, int ksize) {
+  struct Cand { int bm, bn; double eff; int waves, resident; };
+  const Cand cands[] = {{128, 128, 1.0, 4, 2}, {128, 160, 1.2, 4, 2}, {128, 64, 0.72, 4, 2}, {64, 64, 0.42, 4, 4},
+                        {128, 32, 0.36, 4, 4}, {256, 256, 1.5, 8, 1}};
   TileCfg best{128, 128, 1};
   double best_t = 1e300;
   for (const Cand& c : cands) {
     if (c.bn == 32 && N > 32) continue;
     if (N <= 32 && c.bn != 32) continue;
-    // 256x256 pays off on wide N (GEGLU W1, fused q|k|v at 1280 channels) or when
-    // 160 does not divide N (the VAE's 512); measured with scripts/gemm_bench.py
-    if (c.bm == 256 && (!big_ok || (N % 256 != 0 && N < 1920) || (N <= 1280 && N % 160 == 0))) continue;
+    if (c.bm == 256) {
+      if (!big_ok || N < 256) continue;
+      // linears: 256x256 only on wide N (GEGLU W1, fused q|k|v at 1280 channels) or when
+      // 160 does not divide N (the VAE's 512); 3x3 convs: the cost model decides
+      if (ksize == 1 && ((N % 256 != 0 && N < 1920) || (N <= 1280 && N % 160 == 0))) continue;
+    }
     if (c.bn == 160 && N % 160 != 0) continue;  // the UNet's widths are all multiples of 160
     const long tiles = (long)cdiv(M, c.bm) * cdiv(N, c.bn);
-    for (int split = 1; split <= 16; split *= 2) {
-      if (split > 1 && (!allow_split || ktiles / split < 4)) break;
+    for (int split = 1; split <= 16; ++split) {
+      // split-K only to fill the chip (grids of fewer tiles than CUs)
+      if (split > 1 && (!allow_split || ktiles / split < 4 || tiles >= 256)) break;
       const long blocks = tiles * split;
+      const long per_cu = (blocks + 255) / 256;
+      const long conc = std::min<long>(c.resident, per_cu);
+      const double f = (c.waves * conc >= 8) ? 1.0 : 0.75;
       const double per_block = (double)c.bm * c.bn * 64.0 * cdiv(ktiles, split) / c.eff;
-      double t = std::max(1.0, blocks / 256.0) * per_block;
-      if (split > 1) t += (double)M * N * split * 8.0;  // fp32 slab write + read: bytes at chip BW ~ MACs at CU rate
+      double t = per_cu * per_block / f;
+      if (split > 1) t += (double)M * N * split * 1.5;
       if (t < best_t * 0.97) { best_t = t; best = {c.bm, c.bn, split}; }
     }
   }
@@ -1664,7 +1675,7 @@ static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split
   a.ablate = g_ablate;
   a.ktiles = d->K / 64;
   t = pick_tile(M, d->N, a.ktiles, d->split_k <= 0 && d->workspace != nullptr,
-                !d->aff_scale && !g_force_regstage && (d->ksize == 1 || Cin % 64 == 0));
+                !d->aff_scale && !g_force_regstage && (d->ksize == 1 || Cin % 64 == 0), d->ksize);
   if (g_force_tile) {
     static const int tb[11][2] = {{0, 0}, {128, 128}, {128, 64}, {64, 64}, {128, 32}, {256, 256}, {256, 128},
                                   {257, 256}, {258, 256}, {128, 160}, {259, 160}};
