@@ -8,6 +8,8 @@
   slp_noasm  slp_bw + the row-block kernel's remaining inline asm (lgkmcnt waits and
           compiler memory barriers around s_barrier) replaced by __syncthreads(): the
           kernel then holds no hand-written asm at all;
+  slp_nop slp + `-mllvm -amdgpu-snop-padding=4` (s_nop 4 before every instruction);
+  slp_wz  slp + `-mllvm -amdgpu-waitcnt-forcezero` (every wait drains all counters);
   slp_sb  slp + a scheduling barrier right after the row-block LayerNorm loop, so
           the packed normalisation stays ahead of the first chunk's LDS reads/MFMAs
           instead of being interleaved with them.
@@ -33,7 +35,7 @@ WAIT_BUILTIN = ("template <int N> __device__ __forceinline__ void wait_vm() "
 LN_END = "  wait_vm<0>();\n  __builtin_amdgcn_s_barrier();\n  asm volatile(\"\" ::: \"memory\");\n\n  f32x4 acc0[FM][FN]"
 
 
-def variant(name, src):
+def variant(name, src, extra=()):
     top = os.path.join(OUT, name)
     shutil.rmtree(top, ignore_errors=True)
     d = os.path.join(top, "pkg", "csrc")  # csrc/../../include/ls_hip.h resolves as in-tree
@@ -46,7 +48,7 @@ def variant(name, src):
     for fn in sorted(os.listdir(d)):
         if not fn.endswith(".hip"):
             continue
-        flags = FLAGS + ([] if fn == "ls_gemm.hip" else ["-fno-slp-vectorize"])
+        flags = FLAGS + (list(extra) if fn == "ls_gemm.hip" else ["-fno-slp-vectorize"])
         o = os.path.join(d, fn[:-4] + ".o")
         procs.append(subprocess.Popen([HIPCC] + flags + ["-c", os.path.join(d, fn), "-o", o]))
         objs.append(o)
@@ -55,7 +57,7 @@ def variant(name, src):
     lib = os.path.join(ROOT, "latentsync_amd", f"libls_hip_{name}.so")
     subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib] + objs)
     # device disassembly of the LN-folded row-block kernel (FLAGS = RB_LN)
-    s = subprocess.run([HIPCC] + FLAGS + ["--cuda-device-only", "-S",
+    s = subprocess.run([HIPCC] + FLAGS + list(extra) + ["--cuda-device-only", "-S",
                         os.path.join(d, "ls_gemm.hip"), "-o", "-"], capture_output=True, text=True).stdout
     sym = "_ZN2ls20gemm_rowblock_kernelILi10ELi2ELi2ELi1EEEvNS_8ConvArgsE:"
     body = s[s.index(sym):]
@@ -70,7 +72,7 @@ def main():
     if only:
         global variant
         build = variant
-        variant = lambda name, src: build(name, src) if name in only else None
+        variant = lambda name, src, extra=(): build(name, src, extra) if name in only else None
     base = open(os.path.join(CSRC, "ls_gemm.hip")).read()
     assert WAIT_ASM in base and base.count(LN_END) == 1
     os.makedirs(OUT, exist_ok=True)
@@ -82,6 +84,12 @@ def main():
     assert base.count(rb_sync) == 1 and base.count(ln_sync) == 1
     noasm = base.replace(WAIT_ASM, WAIT_BUILTIN).replace(rb_sync, "    __syncthreads();\n  };")
     variant("slp_noasm", noasm.replace(ln_sync, "  __syncthreads();\n\n  f32x4 acc0[FM][FN]"))
+    # compiler-side knobs on the unchanged source: 4 wait states before every
+    # instruction (a VALU / MFMA hazard that needs more nops than the compiler
+    # inserts disappears), and every s_waitcnt forced to zero (a memory-counter race
+    # disappears)
+    variant("slp_nop", base, ["-mllvm", "-amdgpu-snop-padding=4"])
+    variant("slp_wz", base, ["-mllvm", "-amdgpu-waitcnt-forcezero"])
     variant("slp_sb", base.replace(LN_END, LN_END.replace("  wait_vm<0>();\n", "  __builtin_amdgcn_sched_barrier(0);\n  wait_vm<0>();\n", 1)))
 
 
