@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LS_ABI_VERSION 6
+#define LS_ABI_VERSION 7
 
 typedef enum {
   LS_OK = 0,
@@ -101,9 +101,23 @@ typedef struct {
                                 kernel emits them from its epilogue, other paths run
                                 ls_row_stats on y)                                  */
   float row_stats_eps;       /* LayerNorm eps of row_stats_out (0 = 1e-5)        */
+  float* gn_colsum_out;      /* NULL or fp32 [M / LS_GN_SLOT_ROWS][2][N]: per 128-row slot and
+                                output column, the sum and the sum of squares of the stored
+                                bf16 values (GroupNorm statistics of y for
+                                ls_groupnorm_colsum; M % 128 == 0, bf16 output, no GEGLU).
+                                The tiled kernels emit them from their epilogue; the other
+                                paths (split-K, row-block, small tiles) read y once more. */
 } ls_conv_desc;
 
+#define LS_GN_SLOT_ROWS 128
+
 int ls_conv2d(const ls_conv_desc* d, void* stream);
+/* Which kernel family ls_conv2d would run for d: 0 = tiled DMA GEMM, 1 = row-block
+ * GEMM (K = 320 / 640 linears; also takes the GroupNorm affine prologue on its
+ * register-resident A rows), 2 = register-staged tiled GEMM (affine prologue
+ * elsewhere -- callers materialise the affine with ls_groupnorm_apply instead),
+ * -1 = invalid descriptor.  Host-only, no launch. */
+int ls_conv_path(const ls_conv_desc* d);
 size_t ls_conv_workspace_bytes(const ls_conv_desc* d);
 
 /*
@@ -122,6 +136,22 @@ int ls_groupnorm(const uint16_t* x1, const uint16_t* x2, int32_t C1, int32_t C2,
                  int64_t pix_per_sample, int32_t groups, float eps, const float* gamma, const float* beta,
                  float* scale, float* shift, void* workspace, size_t workspace_bytes, void* stream);
 size_t ls_groupnorm_workspace_bytes(int32_t n_samples, int32_t groups);
+
+/*
+ * GroupNorm statistics from producer column sums (ls_conv_desc.gn_colsum_out or
+ * ls_gn_colsum): the same affine as ls_groupnorm without reading the activation
+ * again.  cs1 / cs2: [n_samples * pix_per_sample / 128][2][C1 | C2] of x1 / x2;
+ * pix_per_sample % LS_GN_SLOT_ROWS == 0.  Slot sums are merged in fp64 per
+ * (sample, group); var = E[x^2] - mean^2 (the fp32 slot sums bound the relative
+ * variance error by ~1e-7 * (1 + mean^2 / var)).
+ */
+int ls_groupnorm_colsum(const float* cs1, const float* cs2, int32_t C1, int32_t C2, int32_t n_samples,
+                        int64_t pix_per_sample, int32_t groups, float eps, const float* gamma, const float* beta,
+                        float* scale, float* shift, void* stream);
+
+/* The column sums of an existing bf16 [M][ldy] tensor (first N columns) by a read
+ * pass: out [M / 128][2][N] as ls_conv_desc.gn_colsum_out. */
+int ls_gn_colsum(const uint16_t* y, int64_t ldy, int64_t M, int32_t N, float* out, void* stream);
 
 /* Materialised GroupNorm(+SiLU) apply over an optional channel concat
  * (x1 | x2) -> y [n_pix][C1 + C2]: the input of a 3x3 conv, whose gather would

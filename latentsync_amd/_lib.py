@@ -10,7 +10,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LS_HIP_LIB", os.path.join(HERE, "libls_hip.so"))
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 c_u16p = C.c_void_p
 c_vp = C.c_void_p
@@ -35,6 +35,7 @@ class ConvDesc(C.Structure):
         ("workspace", c_vp), ("workspace_bytes", C.c_size_t),
         ("ln_rowstats", c_vp), ("ln_colsum", c_vp), ("rowvec_mod", C.c_int32),
         ("row_stats_out", c_vp), ("row_stats_eps", C.c_float),
+        ("gn_colsum_out", c_vp),
     ]
 
 
@@ -52,9 +53,13 @@ _SIGS = {
     "ls_last_error": (C.c_char_p, []),
     "ls_conv2d": (C.c_int, [C.POINTER(ConvDesc), c_vp]),
     "ls_conv_workspace_bytes": (C.c_size_t, [C.POINTER(ConvDesc)]),
+    "ls_conv_path": (C.c_int, [C.POINTER(ConvDesc)]),
     "ls_groupnorm": (C.c_int, [c_vp, c_vp, C.c_int32, C.c_int32, C.c_int32, C.c_int64, C.c_int32, C.c_float,
                                c_vp, c_vp, c_vp, c_vp, c_vp, C.c_size_t, c_vp]),
     "ls_groupnorm_workspace_bytes": (C.c_size_t, [C.c_int32, C.c_int32]),
+    "ls_groupnorm_colsum": (C.c_int, [c_vp, c_vp, C.c_int32, C.c_int32, C.c_int32, C.c_int64, C.c_int32, C.c_float,
+                                      c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "ls_gn_colsum": (C.c_int, [c_vp, C.c_int64, C.c_int64, C.c_int32, c_vp, c_vp]),
     "ls_groupnorm_apply": (C.c_int, [c_vp, c_vp, C.c_int32, C.c_int32, C.c_int64, C.c_int64, c_vp, c_vp, C.c_int32,
                                      c_vp, c_vp]),
     "ls_layernorm": (C.c_int, [c_vp, C.c_int64, C.c_int64, C.c_int32, C.c_float, c_vp, c_vp, c_vp, C.c_int32, C.c_int32,

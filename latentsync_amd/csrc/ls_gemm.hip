@@ -31,6 +31,7 @@ struct ConvArgs {
   int ktiles, kt_per_split, split; float* partial;
   int ntm, ntn;
   float* stats_out; float stats_eps;  // row (mean, rstd) of y (row-block epilogue or a trailing row_stats)
+  float* cs_out;  // GroupNorm column sums of y: [M / CS_ROWS][2][N] fp32 (sum, sum of squares per slot)
   int ablate;  // tuning only (bits): 2 = skip operand DMA, 4 = skip epilogue stores, 8 = skip epilogue,
                // 16 = skip MFMAs (DMA kernel)
 };
@@ -203,6 +204,20 @@ __device__ __forceinline__ void stage_acc(f32x4 (&acc)[BM / WM / 16][BN / WN / 1
 // per-row side inputs (residual, row vector, LayerNorm row stats) of all of a
 // thread's rows in a wave-row pass are issued together before any is consumed --
 // one L2/HBM round trip per pass instead of one per chunk.
+// GroupNorm statistics from the producer (a.cs_out): per CS_ROWS-row slot and column,
+// the sum and the sum of squares of the STORED (bf16-rounded) values, fp32 over the
+// slot -- what gn_stats_kernel would read back; ls_groupnorm_colsum merges the slots
+// of a sample in fp64.  The store loop writes the rounded values back over its fp32
+// staging; after the pass barrier one thread per column adds the pass's rows from LDS
+// (2 registers across passes -- the 256x256 kernel is at its VGPR limit), then a
+// barrier before the next pass re-stages.  A slot's sums go out with its last pass.
+constexpr int CS_ROWS = LS_GN_SLOT_ROWS;
+
+template <int BM, int BN, int WM, int WN>
+__host__ __device__ constexpr bool cs_tile_fits() {
+  return BM % CS_ROWS == 0 && CS_ROWS % (BM / WM) == 0 && WM * WN * 64 >= BN;
+}
+
 template <int BM, int BN, int WM, int WN, bool GEN>
 __device__ __forceinline__ void store_tile_plain(const ConvArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
                                                  float* st, int m0, int n0) {
@@ -210,10 +225,13 @@ __device__ __forceinline__ void store_tile_plain(const ConvArgs& a, f32x4 (&acc)
   constexpr int CPRW = BN / 8;                 // chunk columns per tile row
   constexpr int RPI = NT / CPRW;               // rows per iteration
   constexpr int ITER = (WTM + RPI - 1) / RPI;  // iterations per wave-row pass
+  constexpr bool CSOK = cs_tile_fits<BM, BN, WM, WN>();
   const int tid = threadIdx.x;
   const int c8 = (tid % CPRW) * 8, r0 = tid / CPRW;
   const int col = n0 + c8;
   const bool cok = (r0 < RPI) && col < a.N;
+  const bool cs_on = CSOK && a.cs_out != nullptr;
+  float g1 = 0.f, g2 = 0.f;  // column tid's sums over the slot's passes so far
   // row vector (per-frame temb / positional-encoding rows): one row for the whole
   // tile in the common case (rows_per_vec >= the tile's row span), folded into
   // the per-column constants; otherwise looked up per row.
@@ -270,10 +288,42 @@ __device__ __forceinline__ void store_tile_plain(const ConvArgs& a, f32x4 (&acc)
         *(float4*)y = make_float4(v[0], v[1], v[2], v[3]);
         *(float4*)(y + 4) = make_float4(v[4], v[5], v[6], v[7]);
       } else {
-        *(uint4*)((u16*)a.y + (long)row * a.ldy + col) = pack8(v);
+        const uint4 pk = pack8(v);
+        *(uint4*)((u16*)a.y + (long)row * a.ldy + col) = pk;
+        if (cs_on) {  // the stored values replace their fp32 staging
+          float b[8];
+          unpack8(pk, b);
+          float* sw = st + rl * SP + c8;
+          *(float4*)sw = make_float4(b[0], b[1], b[2], b[3]);
+          *(float4*)(sw + 4) = make_float4(b[4], b[5], b[6], b[7]);
+        }
       }
     }
     __syncthreads();
+    if (cs_on) {  // (block-uniform)
+      const bool mine = tid < BN && n0 + tid < a.N;
+      if (mine) {
+        float t1 = 0.f, t2 = 0.f;
+#pragma unroll 8
+        for (int r = 0; r < WTM; ++r) {
+          const float x = st[r * SP + tid];
+          t1 += x;
+          t2 = fmaf(x, x, t2);
+        }
+        g1 += t1;
+        g2 += t2;
+      }
+      if (((p + 1) * WTM) % CS_ROWS == 0) {  // the slot is complete
+        if (mine) {
+          float* o = a.cs_out + (m0 + (long)p * WTM) / CS_ROWS * 2 * a.N + n0 + tid;
+          o[0] = g1;
+          o[a.N] = g2;
+        }
+        g1 = 0.f;
+        g2 = 0.f;
+      }
+      __syncthreads();
+    }
   }
 }
 
@@ -1173,6 +1223,52 @@ __global__ void splitk_reduce_kernel(ConvArgs a) {
   }
 }
 
+// GroupNorm column sums of a stored bf16 [M][ldy] tensor by a separate read pass
+// (producers whose epilogue does not emit them: split-K, the row-block kernel, the
+// small tiles).  Block = (slot, 32 column chunks of 8); thread = (chunk, row lane of
+// 8); same fp32-per-slot sums as the epilogue (the order of the adds differs).
+__global__ void __launch_bounds__(256) colsum_pass_kernel(const u16* __restrict__ y, long ldy, int N,
+                                                          float* __restrict__ out) {
+  __shared__ float red[8][32][17];
+  const int lane = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const long slot = blockIdx.x;
+  const int cc = blockIdx.y * 32 + lane;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  if (cc * 8 < N) {
+    const u16* src = y + slot * CS_ROWS * ldy + cc * 8;
+#pragma unroll 4
+    for (int r = rl; r < CS_ROWS; r += 8) {
+      float f[8];
+      unpack8(*(const uint4*)(src + (long)r * ldy), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { s1[j] += f[j]; s2[j] = fmaf(f[j], f[j], s2[j]); }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[rl][lane][j] = s1[j]; red[rl][lane][8 + j] = s2[j]; }
+  __syncthreads();
+  if (rl == 0 && cc * 8 < N) {
+    float t[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t[j] = red[0][lane][j];
+    for (int k = 1; k < 8; ++k)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) t[j] += red[k][lane][j];
+    float* o = out + slot * 2 * N + cc * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { o[j] = t[j]; o[N + j] = t[8 + j]; }
+  }
+}
+
+static int launch_colsum_pass(const u16* y, long ldy, long M, int N, float* out, hipStream_t s) {
+  if (!y || !out || M <= 0 || M % CS_ROWS || N <= 0 || N % 8 || ldy % 8)
+    return fail(LS_ERR_INVALID, "gn column sums: M % 128 == 0, N % 8 == 0, ldy % 8 == 0");
+  colsum_pass_kernel<<<dim3((unsigned)(M / CS_ROWS), cdiv(N / 8, 32)), 256, 0, s>>>(y, ldy, N, out);
+  return check_launch("colsum_pass_kernel");
+}
+
 // ------------------------------------------------------------ row-block GEMM
 // The short-K linears of the 32x32 level (K = Cin = 320: Transformer/motion
 // proj_in/out, fused q|k|v, q, out-proj, GEGLU W1) are epilogue/bandwidth bound
@@ -1195,7 +1291,25 @@ __global__ void splitk_reduce_kernel(ConvArgs a) {
 // Host contract (rowblock_ok): ksize 1, no x2 / affine prologue, K = 32*KT = Cin
 // (320 with FM = 2: 256 rows per block; 640 with FM = 1: 128 rows, A still 80 VGPRs),
 // M % BM == 0, N % 64 == 0, no split-K, bf16 output with 4-aligned pitches.
-enum { RB_LN = 1, RB_RES = 2, RB_RV = 4, RB_GEGLU = 8, RB_STATS = 16 };
+enum { RB_LN = 1, RB_RES = 2, RB_RV = 4, RB_GEGLU = 8, RB_STATS = 16, RB_GNCS = 32, RB_AFF = 64 };
+
+// sum over the 16 lanes of a DPP row (all 16 receive it): quad butterflies, then
+// rotations by 4 and 8 within the row
+__device__ __forceinline__ float row16_sum(float v) {
+  auto dpp = [](float x, int ctrl) -> float {
+    switch (ctrl) {  // dpp_ctrl must be a constant
+      case 0: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));
+      case 1: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));
+      case 2: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x124, 0xF, 0xF, false));
+      default: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x128, 0xF, 0xF, false));
+    }
+  };
+  v += dpp(v, 0);
+  v += dpp(v, 1);
+  v += dpp(v, 2);
+  v += dpp(v, 3);
+  return v;
+}
 
 template <int KT, int FM, int FN, int FLAGS>
 __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
@@ -1205,7 +1319,13 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
   constexpr int WIMG = BN * KTILES * 8;       // uint4 of the W images of a chunk
   constexpr int STAGE = WIMG + 48;            // + bias / colsum / row-vector columns (3 x 64 fp32)
   constexpr bool LN = FLAGS & RB_LN, RES = FLAGS & RB_RES, RV = FLAGS & RB_RV, GG = FLAGS & RB_GEGLU;
+  constexpr bool AF = FLAGS & RB_AFF;  // GroupNorm affine (+SiLU) prologue on the register-resident A rows
   constexpr bool ST = (FLAGS & RB_STATS) && !GG;  // row statistics of the output (host: one N range per block)
+  // GroupNorm column sums (a.cs_out): per chunk a wave's 16 FM rows are summed over its
+  // lanes (DPP) into LDS; after the chunk's barrier the CS_ROWS / (16 FM) waves of a
+  // slot are added in a fixed order and written (host: BM % CS_ROWS == 0)
+  constexpr bool CS = (FLAGS & RB_GNCS) && !GG;
+  constexpr int WPS = CS_ROWS / (16 * FM);  // waves per 128-row slot
   constexpr int NSTORE = GG ? FM * FN / 2 : FM * FN;
   constexpr int PPT = (WIMG + 511) / 512;     // 16-B DMA pieces per thread per chunk
   static_assert(KT % 2 == 0 && WIMG % 256 == 0, "K must be a multiple of 64");
@@ -1270,6 +1390,29 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
       }
     }
   }
+  if (AF) {
+    // x * scale[s][c] + shift[s][c] (+ SiLU), rounded to bf16 like ls_groupnorm_apply's
+    // materialised output; the block's rows lie in one sample (host: pix_per_sample % BM == 0)
+    const long sb = (long)((rb * BM) / a.pix_per_sample) * a.Cin + lg * 8;
+    wait_vm<0>();
+#pragma unroll
+    for (int s = 0; s < KT; ++s) {
+      float sc[8], sh[8];
+      load8f(a.aff_scale + sb + s * 32, sc);
+      load8f(a.aff_shift + sb + s * 32, sh);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        bf16x8 v = ar[i][s];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float t = fmaf((float)v[e], sc[e], sh[e]);
+          if (a.silu_in) t = silu(t);
+          v[e] = (__bf16)t;
+        }
+        ar[i][s] = v;
+      }
+    }
+  }
   wait_vm<0>();
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
@@ -1306,6 +1449,7 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
   auto epilogue = [&](int c, const float4 (&bb)[FN], f32x4 (&acc)[FM][FN], const uint2 (&rs)[FM][FN]) {
     const int nb = c * BN + 4 * lg;  // packed column of fragment j: nb + 16 j
     float cs1[FM], cs2[FM];  // this chunk's partial sums (fp32 over 4*FN values), folded into S in fp64
+    float gcs[FM][FN][4];    // stored values of this chunk (CS)
 #pragma unroll
     for (int i = 0; i < FM; ++i) { cs1[i] = 0.f; cs2[i] = 0.f; }
 #pragma unroll
@@ -1336,6 +1480,10 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
           for (int r = 0; r < 4; ++r) o[r] = (acc[i][j][r] + r4[r]) * a.out_scale;
           const uint2 pk = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
           *(uint2*)(yrow + nb + 16 * j) = pk;
+          if (CS) {
+            gcs[i][j][0] = __uint_as_float(pk.x << 16); gcs[i][j][1] = __uint_as_float(pk.x & 0xffff0000u);
+            gcs[i][j][2] = __uint_as_float(pk.y << 16); gcs[i][j][3] = __uint_as_float(pk.y & 0xffff0000u);
+          }
           if (ST) {  // statistics of the stored (bf16-rounded) values, like ls_row_stats reads them
             const float b0 = __uint_as_float(pk.x << 16), b1 = __uint_as_float(pk.x & 0xffff0000u);
             const float b2 = __uint_as_float(pk.y << 16), b3 = __uint_as_float(pk.y & 0xffff0000u);
@@ -1348,6 +1496,37 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
     if (ST) {
 #pragma unroll
       for (int i = 0; i < FM; ++i) { S1[i] += (double)cs1[i]; S2[i] += (double)cs2[i]; }
+    }
+    if (CS) {  // column sums of this wave's rows -> LDS part[c & 1][wave][64]
+      float* part = (float*)(lds_dyn + 3 * STAGE) + (c & 1) * 512 + wid * 64;
+      float mine = 0.f;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {  // v = kind * 8 + j * 4 + r
+        const int j = (v >> 2) & 1, r = v & 3;
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const float b = gcs[i][j][r];
+          t += (v >> 3) ? b * b : b;
+        }
+        t = row16_sum(t);
+        mine = (l16 == v) ? t : mine;
+      }
+      // lane (lg, l16): column 4 lg + 16 j + r of the chunk, value kind
+      const int v = l16, col = 4 * lg + 16 * ((v >> 2) & 1) + (v & 3);
+      part[col * 2 + (v >> 3)] = mine;
+    }
+  };
+  // slots of this block's rows: add the WPS waves of each for chunk cc and write them
+  auto merge_cs = [&](int cc) {
+    const float* part = (const float*)(lds_dyn + 3 * STAGE) + (cc & 1) * 512;
+    for (int q = tid; q < (BM / CS_ROWS) * 64; q += 512) {
+      const int sl = q >> 6, e = q & 63;
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < WPS; ++w) t += part[(sl * WPS + w) * 64 + e];
+      const long slot = (long)rb * (BM / CS_ROWS) + sl;
+      a.cs_out[slot * 2 * a.N + (e & 1) * a.N + cc * BN + (e >> 1)] = t;
     }
   };
   auto mfma_chunk = [&](int stage, f32x4 (&acc)[FM][FN]) {
@@ -1386,6 +1565,7 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
     float4 bb[FN];
     load_prm(st == 0 ? 2 : st - 1, bb);
     issue(min(c + 1, c1 - 1), st == 2 ? 0 : st + 1);
+    if (CS && c - 2 >= c0) merge_cs(c - 2);  // written two epilogues ago, past a barrier
     load_res(c, rs_load);
     mfma_chunk(st, acc);
     epilogue(c - 1, bb, prev, rs_use);
@@ -1411,6 +1591,10 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
   } else {
     load_prm((c1 - 1 - c0) % 3, bb);
     epilogue(c1 - 1, bb, acc0, rsA);
+  }
+  if (CS) {  // the last two chunks' column sums
+    __syncthreads();
+    for (int cc = max(c0, c1 - 2); cc < c1; ++cc) merge_cs(cc);
   }
   if (ST) {  // the 4 lane groups of a row hold disjoint column slices: combine, then lane group 0 writes
 #pragma unroll
@@ -1482,7 +1666,11 @@ static bool g_rowblock = getenv("LS_GEMM_NO_ROWBLOCK") == nullptr;
 static bool g_rowblock640 = getenv("LS_GEMM_NO_ROWBLOCK640") == nullptr;
 
 static bool rowblock_ok(const ls_conv_desc* d, const ConvArgs& a) {
-  if (!g_rowblock || g_force_tile || g_force_regstage || d->ksize != 1 || a.C2 || a.aff_scale) return false;
+  if (!g_rowblock || g_force_tile || g_force_regstage || d->ksize != 1 || a.C2) return false;
+  // GroupNorm affine prologue: one sample per block, and not together with the LayerNorm fold
+  if (a.aff_scale && (a.ln_mr || a.pix_per_sample % (a.Cin == 320 ? 256 : 128) ||
+                      ((uintptr_t)a.aff_scale | (uintptr_t)a.aff_shift) & 15))
+    return false;
   // K = 640 only without a residual (the tiled kernel is faster there: 48 vs 53 us at 16x16)
   if (!((a.Cin == 320 && a.K == 320 && a.M % 256 == 0) ||
         (g_rowblock640 && a.Cin == 640 && a.K == 640 && a.M % 128 == 0 && !a.res)))
@@ -1499,7 +1687,7 @@ static bool rowblock_ok(const ls_conv_desc* d, const ConvArgs& a) {
 template <int KT, int FM, int FLAGS>
 static void launch_rowblock2(const ConvArgs& a, int grid, hipStream_t s) {
   constexpr int FN = 2;
-  const size_t shm = (size_t)3 * (16 * FN * (KT / 2) * 8 + 48) * 16;
+  const size_t shm = (size_t)3 * (16 * FN * (KT / 2) * 8 + 48) * 16 + ((FLAGS & RB_GNCS) ? 4096 : 0);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gemm_rowblock_kernel<KT, FM, FN, FLAGS>,
@@ -1516,15 +1704,30 @@ static void launch_rowblock1(const ConvArgs& a, int grid, hipStream_t s) {
 }
 
 // returns false when no instance matches (the caller then uses the tiled kernels)
-static bool launch_rowblock(ConvArgs& a, hipStream_t s) {
+// compiled row-block instances (FLAGS combinations)
+static const int kRowblockInstances[] = {0, RB_LN, RB_LN | RB_RV, RB_RES, RB_LN | RB_RES, RB_LN | RB_GEGLU, RB_GEGLU,
+                                         RB_STATS, RB_RES | RB_STATS, RB_RES | RB_GNCS, RB_AFF, RB_AFF | RB_STATS};
+
+// the row-block instance flags for this call, or -1 (sets a.ntm / a.ntn)
+static int rowblock_flags(ConvArgs& a) {
   const int bm = a.K == 320 ? 256 : 128;
   const int ntm = a.M / bm, nch = a.N / 32;
   a.ntm = ntm;
   a.ntn = std::max(1, std::min(nch, (256 + ntm - 1) / ntm));
-  if (a.stats_out && a.ntn != 1) return false;  // fused statistics need whole rows per block
+  if (a.stats_out && a.ntn != 1) return -1;  // fused statistics need whole rows per block
+  if (a.cs_out && (bm % CS_ROWS || a.ntn != 1)) return -1;
   const int flags = (a.ln_mr ? RB_LN : 0) | (a.res ? RB_RES : 0) | (a.rowvec ? RB_RV : 0) |
-                    (a.act == LS_ACT_GEGLU ? RB_GEGLU : 0) | (a.stats_out ? RB_STATS : 0);
-  const int grid = ntm * a.ntn;
+                    (a.act == LS_ACT_GEGLU ? RB_GEGLU : 0) | (a.stats_out ? RB_STATS : 0) | (a.cs_out ? RB_GNCS : 0) |
+                    (a.aff_scale ? RB_AFF : 0);
+  for (int f : kRowblockInstances)
+    if (f == flags) return flags;
+  return -1;
+}
+
+// returns false when no instance matches (the caller then uses the tiled kernels)
+static bool launch_rowblock(ConvArgs& a, hipStream_t s) {
+  const int flags = rowblock_flags(a);
+  const int grid = a.ntm * a.ntn;
   switch (flags) {
     case 0: launch_rowblock1<0>(a, grid, s); return true;
     case RB_LN: launch_rowblock1<RB_LN>(a, grid, s); return true;
@@ -1535,6 +1738,9 @@ static bool launch_rowblock(ConvArgs& a, hipStream_t s) {
     case RB_GEGLU: launch_rowblock1<RB_GEGLU>(a, grid, s); return true;
     case RB_STATS: launch_rowblock1<RB_STATS>(a, grid, s); return true;
     case RB_RES | RB_STATS: launch_rowblock1<RB_RES | RB_STATS>(a, grid, s); return true;
+    case RB_RES | RB_GNCS: launch_rowblock1<RB_RES | RB_GNCS>(a, grid, s); return true;
+    case RB_AFF: launch_rowblock1<RB_AFF>(a, grid, s); return true;
+    case RB_AFF | RB_STATS: launch_rowblock1<RB_AFF | RB_STATS>(a, grid, s); return true;
     default: return false;
   }
 }
@@ -1672,6 +1878,9 @@ static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split
   a.stats_eps = d->row_stats_eps > 0.f ? d->row_stats_eps : 1e-5f;
   if (a.stats_out && (d->ksize != 1 || d->act == LS_ACT_GEGLU || d->y_f32))
     return fail(LS_ERR_INVALID, "ls_conv2d: row_stats_out needs ksize 1, bf16 output, no GEGLU");
+  a.cs_out = d->gn_colsum_out;
+  if (a.cs_out && (M % CS_ROWS || d->N % 8 || d->ldy % 8 || d->act == LS_ACT_GEGLU || d->y_f32))
+    return fail(LS_ERR_INVALID, "ls_conv2d: gn_colsum_out needs M % 128 == 0, N % 8 == 0, bf16 output, no GEGLU");
   a.ablate = g_ablate;
   a.ktiles = d->K / 64;
   t = pick_tile(M, d->N, a.ktiles, d->split_k <= 0 && d->workspace != nullptr,
@@ -1751,7 +1960,16 @@ extern "C" int ls_conv2d(const ls_conv_desc* d, void* stream) {
     if (split > 1) a.partial = (float*)d->workspace;
   }
   hipStream_t s = (hipStream_t)stream;
-  if (rowblock_ok(d, a) && launch_rowblock(a, s)) return check_launch("gemm_rowblock_kernel");
+  float* cs = a.cs_out;  // GroupNorm column sums: epilogue (tiled / row-block) or a trailing read pass
+  if (rowblock_ok(d, a)) {
+    if (launch_rowblock(a, s)) return check_launch("gemm_rowblock_kernel");  // with cs_out if given
+    a.cs_out = nullptr;  // no row-block instance with the sums: without them, then a read pass
+    if (cs && launch_rowblock(a, s)) {
+      if ((rc = check_launch("gemm_rowblock_kernel")) != LS_OK) return rc;
+      return launch_colsum_pass((const u16*)d->y, d->ldy, a.M, d->N, cs, s);
+    }
+  }
+  a.cs_out = nullptr;
   if (a.stats_out) {  // tiled path: the GEMM, then LayerNorm statistics of y in a second pass
     float* so = a.stats_out;
     a.stats_out = nullptr;
@@ -1762,6 +1980,11 @@ extern "C" int ls_conv2d(const ls_conv_desc* d, void* stream) {
   }
   const bool tapu = (d->ksize == 3) && (a.Cin % 64 == 0);
   const int grid = a.ntm * a.ntn * a.split;
+  // epilogue column sums: single-pass vectorised epilogue and a tile whose staging
+  // buffer holds the per-thread partials (cs_tile_fits; not 128x32 / 64x64)
+  const bool vec = (a.N % 8 == 0) && (a.ldy % 8 == 0) && (!a.res || a.ldr % 8 == 0);
+  const bool cs_epi = cs && a.split == 1 && vec && !(t.bm == 128 && t.bn == 32) && t.bm != 64;
+  if (cs_epi) a.cs_out = cs;
   if (t.bm == 257 && !a.aff_scale && !g_force_regstage && (d->ksize == 1 || tapu)) {  // phased 256x256
     if (d->ksize == 1) launch_p8_1<1, false>(a, grid, s);
     else launch_p8_1<3, true>(a, grid, s);
@@ -1784,5 +2007,18 @@ extern "C" int ls_conv2d(const ls_conv_desc* d, void* stream) {
     splitk_reduce_kernel<<<cdiv(nchunk, 256), 256, 0, s>>>(a);
     if ((rc = check_launch("splitk_reduce_kernel")) != LS_OK) return rc;
   }
+  if (cs && !cs_epi) return launch_colsum_pass((const u16*)d->y, d->ldy, a.M, d->N, cs, s);
   return LS_OK;
+}
+
+extern "C" int ls_conv_path(const ls_conv_desc* d) {
+  ConvArgs a; TileCfg t; int split;
+  if (build_args(d, a, t, split) != LS_OK) return -1;
+  a.cs_out = nullptr;  // (the column sums never change the path)
+  if (rowblock_ok(d, a) && rowblock_flags(a) >= 0) return 1;
+  return (a.aff_scale || g_force_regstage) ? 2 : 0;
+}
+
+extern "C" int ls_gn_colsum(const uint16_t* y, int64_t ldy, int64_t M, int32_t N, float* out, void* stream) {
+  return launch_colsum_pass(y, ldy, M, N, out, (hipStream_t)stream);
 }

@@ -157,6 +157,45 @@ static int gn_nsplit(int n_samples, long pps, int C) {
   return (int)std::max<long>(1, std::min<long>(ns, 4096));
 }
 
+// GroupNorm statistics from producer column sums (ls_conv_desc.gn_colsum_out):
+// block = (group, sample); the slot sums of the group's channels over the sample's
+// slots are added in fp64 (fixed order per thread, then a fixed-shape tree), so
+// the result does not depend on scheduling.
+__global__ void __launch_bounds__(256)
+gn_colsum_finalize_kernel(const float* __restrict__ cs1, const float* __restrict__ cs2, int C1, int C2,
+                          long slots_per_sample, int groups, float eps, const float* __restrict__ gamma,
+                          const float* __restrict__ beta, float* __restrict__ scale, float* __restrict__ shift) {
+  __shared__ double r1[4], r2[4];
+  const int C = C1 + C2, cpg = C / groups;
+  const int g = blockIdx.x, s = blockIdx.y, tid = threadIdx.x;
+  // thread = (channel of the group, slot lane): no integer division in the loop
+  const int lanes = 256 / cpg, cl = tid % cpg, sl = tid / cpg;
+  double t1 = 0.0, t2 = 0.0;
+  if (sl < lanes) {
+    const int c = g * cpg + cl;
+    const int n = c < C1 ? C1 : C2;
+    const float* p = (c < C1 ? cs1 + c : cs2 + (c - C1)) + (long)s * slots_per_sample * 2 * n;
+    for (long q = sl; q < slots_per_sample; q += lanes) {
+      t1 += (double)p[q * 2 * n];
+      t2 += (double)p[q * 2 * n + n];
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) { t1 += shfl_xor_d(t1, off); t2 += shfl_xor_d(t2, off); }
+  if ((tid & 63) == 0) { r1[tid >> 6] = t1; r2[tid >> 6] = t2; }
+  __syncthreads();
+  if (tid < cpg) {
+    const double s1 = (r1[0] + r1[1]) + (r1[2] + r1[3]), s2 = (r2[0] + r2[1]) + (r2[2] + r2[3]);
+    const double n = (double)slots_per_sample * LS_GN_SLOT_ROWS * cpg;
+    const double mean = s1 / n;
+    const double var = fmax(s2 / n - mean * mean, 0.0);
+    const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+    const int c = g * cpg + tid;
+    const float sc = (gamma ? gamma[c] : 1.f) * rstd;
+    scale[(long)s * C + c] = sc;
+    shift[(long)s * C + c] = (beta ? beta[c] : 0.f) - (float)mean * sc;
+  }
+}
+
 // Materialised GroupNorm apply (+SiLU) over an optional channel concat.
 __global__ void gn_apply_kernel(const u16* __restrict__ x1, const u16* __restrict__ x2, int C1, int C2, long n_chunks,
                                 long pps, const float* __restrict__ scale, const float* __restrict__ shift, int silu_on,
@@ -276,6 +315,19 @@ extern "C" int ls_groupnorm(const uint16_t* x1, const uint16_t* x2, int32_t C1, 
   gn_stats_kernel<<<dim3(ns, n_samples), GN_THREADS, shm, (hipStream_t)stream>>>(
       x1, x2, C1, C2, pps, ns, groups, eps, gamma, beta, part, counters, scale, shift);
   return check_launch("gn_stats_kernel");
+}
+
+extern "C" int ls_groupnorm_colsum(const float* cs1, const float* cs2, int32_t C1, int32_t C2, int32_t n_samples,
+                                   int64_t pps, int32_t groups, float eps, const float* gamma, const float* beta,
+                                   float* scale, float* shift, void* stream) {
+  const int C = C1 + C2;
+  if (!cs1 || !scale || !shift || n_samples <= 0 || pps <= 0 || groups <= 0 || C1 <= 0 || C2 < 0 || (C2 && !cs2))
+    return fail(LS_ERR_INVALID, "ls_groupnorm_colsum: bad arguments");
+  if (C % groups || C / groups > 256 || pps % LS_GN_SLOT_ROWS)
+    return fail(LS_ERR_INVALID, "ls_groupnorm_colsum: C % groups == 0, C / groups <= 256, pix_per_sample % 128 == 0");
+  gn_colsum_finalize_kernel<<<dim3(groups, n_samples), 256, 0, (hipStream_t)stream>>>(
+      cs1, cs2, C1, C2, pps / LS_GN_SLOT_ROWS, groups, eps, gamma, beta, scale, shift);
+  return check_launch("gn_colsum_finalize_kernel");
 }
 
 extern "C" int ls_groupnorm_apply(const uint16_t* x1, const uint16_t* x2, int32_t C1, int32_t C2, int64_t n_pix,

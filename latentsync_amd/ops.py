@@ -14,6 +14,7 @@ from . import _lib
 from ._lib import check
 
 ACT_NONE, ACT_GEGLU, ACT_GELU, ACT_SILU = 0, 1, 2, 3
+GN_SLOT_ROWS = 128  # LS_GN_SLOT_ROWS
 
 
 def _p(t):
@@ -71,11 +72,16 @@ def _ld(t):
 
 def conv(x, pw: Packed, *, x2=None, aff=None, stride=1, pad=None, upsample=False, out_hw=None, rowvec=None,
          res=None, out_scale=1.0, act=ACT_NONE, out=None, out_f32=False, split_k=0, ln_stats=None,
-         stats_out=None):
+         stats_out=None, gn_out=False, aff_materialize=False):
     """Fused conv/linear.  x (n, H, W, C1) [+ x2 (n, H, W, C2)] -> (n, Ho, Wo, n_out).
     aff = (scale[S][C], shift[S][C], imgs_per_sample, silu); rowvec = (t[S][ld], rows_per_vec, ld[, mod]);
     ln_stats = (mean, rstd) rows from row_stats(): LayerNorm folded into pw (pw.colsum);
-    stats_out = fp32 (rows, 2) receiving row_stats() of the output (eps 1e-5)."""
+    stats_out = fp32 (rows, 2) receiving row_stats() of the output (eps 1e-5);
+    gn_out = also emit the output's GroupNorm column sums (ls_conv_desc.gn_colsum_out),
+    attached to the result as `.gn_cs` for group_norm() (when rows % 128 == 0);
+    aff_materialize = when the call would take the register-staged GEMM for the affine
+    prologue (ls_conv_path 2), apply it with ls_groupnorm_apply first instead (the
+    row-block GEMM folds it into its register-resident A rows)."""
     lib = _lib.load()
     n, H, W, C1 = x.shape
     C2 = x2.shape[3] if x2 is not None else 0
@@ -120,8 +126,20 @@ def conv(x, pw: Packed, *, x2=None, aff=None, stride=1, pad=None, upsample=False
         assert stats_out.dtype == torch.float32 and stats_out.is_contiguous() and stats_out.numel() == 2 * n * Ho * Wo
         assert pw.n_out == pw.N and act != ACT_GEGLU, "row statistics over the real output channels only"
         d.row_stats_out, d.row_stats_eps = _p(stats_out), 1e-5
+    if aff is not None and aff_materialize and lib.ls_conv_path(C.byref(d)) == 2:
+        xa = group_norm_apply(x, aff[0], aff[1], n // aff[2], bool(aff[3]), x2=x2)
+        return conv(xa, pw, stride=stride, pad=pad, upsample=upsample, out_hw=out_hw, rowvec=rowvec, res=res,
+                    out_scale=out_scale, act=act, out=out, out_f32=out_f32, split_k=split_k, ln_stats=ln_stats,
+                    stats_out=stats_out, gn_out=gn_out)
+    cs = None
+    if gn_out and (n * Ho * Wo) % GN_SLOT_ROWS == 0 and out.dtype == torch.bfloat16 and act != ACT_GEGLU:
+        assert pw.n_out == pw.N
+        cs = torch.empty((n * Ho * Wo // GN_SLOT_ROWS, 2, n_out), dtype=torch.float32, device=x.device)
+        d.gn_colsum_out = _p(cs)
     d.workspace, d.workspace_bytes = _p(ws.gemm), ws.gemm.numel()
     check(lib.ls_conv2d(C.byref(d), _stream()), "ls_conv2d")
+    if cs is not None:
+        out.gn_cs = cs
     return out
 
 
@@ -136,14 +154,41 @@ def linear(x2d, pw: Packed, **kw):
     return y.view(rows, y.shape[-1]) if y.is_contiguous() else y[0, 0]
 
 
+def gn_colsum(x):
+    """Column sums of an existing NHWC bf16 activation (ls_gn_colsum), attached as
+    x.gn_cs -- for GroupNorm inputs no GEMM epilogue produced."""
+    lib = _lib.load()
+    C_ = x.shape[-1]
+    rows = x.numel() // C_
+    cs = torch.empty((rows // GN_SLOT_ROWS, 2, C_), dtype=torch.float32, device=x.device)
+    check(lib.ls_gn_colsum(_p(x), C_, rows, C_, _p(cs), _stream()), "ls_gn_colsum")
+    x.gn_cs = cs
+    return cs
+
+
+def _colsums(x, pps):
+    cs = getattr(x, "gn_cs", None)
+    if cs is None or pps % GN_SLOT_ROWS or not x.is_contiguous():
+        return None
+    C_ = x.shape[-1]
+    return cs if tuple(cs.shape) == (x.numel() // C_ // GN_SLOT_ROWS, 2, C_) else None
+
+
 def group_norm(x, groups, eps, gamma, beta, n_samples, x2=None):
-    """GroupNorm statistics -> (scale, shift) fp32 [n_samples][C]."""
+    """GroupNorm statistics -> (scale, shift) fp32 [n_samples][C].  From the producer's
+    column sums (x.gn_cs, conv(..., gn_out=True)) when present, else a read pass."""
     lib = _lib.load()
     C1 = x.shape[-1]
     C2 = x2.shape[-1] if x2 is not None else 0
     pps = x.numel() // C1 // n_samples
     scale = torch.empty((n_samples, C1 + C2), dtype=torch.float32, device=x.device)
     shift = torch.empty_like(scale)
+    cs1 = _colsums(x, pps)
+    cs2 = _colsums(x2, pps) if x2 is not None else None
+    if cs1 is not None and (x2 is None or cs2 is not None):
+        check(lib.ls_groupnorm_colsum(_p(cs1), _p(cs2), C1, C2, n_samples, pps, groups, eps, _p(gamma), _p(beta),
+                                      _p(scale), _p(shift), _stream()), "ls_groupnorm_colsum")
+        return scale, shift
     ws = workspace(x.device)
     check(lib.ls_groupnorm(_p(x), _p(x2), C1, C2, n_samples, pps, groups, eps, _p(gamma), _p(beta), _p(scale),
                            _p(shift), _p(ws.gn), ws.gn.numel(), _stream()), "ls_groupnorm")

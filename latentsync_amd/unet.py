@@ -131,11 +131,12 @@ class _Resnet:
         pps = F * x.shape[1] * x.shape[2]
         s1 = ops.group_norm(x, self.groups, self.eps, *self.n1, B, x2=x2)
         a1 = ops.group_norm_apply(x, s1[0], s1[1], B, True, x2=x2)
-        h = ops.conv(a1, self.c1, rowvec=(temb_all[:, self.temb_slot:], pps, temb_all.shape[1]))
+        # gn_out: GroupNorm statistics of every GN input come from its producer's epilogue
+        h = ops.conv(a1, self.c1, rowvec=(temb_all[:, self.temb_slot:], pps, temb_all.shape[1]), gn_out=True)
         s2 = ops.group_norm(h, self.groups, self.eps, *self.n2, B)
         a2 = ops.group_norm_apply(h, s2[0], s2[1], B, True)
         res = x if self.sc is None else ops.conv(x, self.sc, x2=x2)
-        return ops.conv(a2, self.c2, res=res, out_scale=self.out_scale)
+        return ops.conv(a2, self.c2, res=res, out_scale=self.out_scale, gn_out=True)
 
 
 class _Transformer:
@@ -166,8 +167,9 @@ class _Transformer:
         sc = ops.group_norm(x, self.groups, 1e-6, *self.norm, n)
         # LayerNorm statistics of every h come out of the GEMM that writes h
         st = torch.empty((rows, 2), dtype=torch.float32, device=x.device)
-        # GN affine materialised (HBM-bound, 2 B/elem each way) so proj_in runs on the DMA GEMM
-        h = ops.conv(ops.group_norm_apply(x, sc[0], sc[1], n, False), self.proj_in, stats_out=st).view(rows, C)
+        # GN affine folded into the row-block GEMM's A rows (32x32 / 16x16); materialised elsewhere
+        h = ops.conv(x, self.proj_in, aff=(sc[0], sc[1], 1, False), aff_materialize=True,
+                     stats_out=st).view(rows, C)
         # self attention (norm1 folded into the q|k|v GEMM)
         qkv = ops.linear(h, self.qkv1, ln_stats=st)
         o = torch.empty((rows, C), dtype=torch.bfloat16, device=x.device)
@@ -187,7 +189,7 @@ class _Transformer:
         # GEGLU feed-forward (norm3 folded)
         g = ops.linear(h, self.ff1, act=ops.ACT_GEGLU, ln_stats=st)
         h = ops.linear(g, self.ff2, res=h)
-        return ops.conv(h.view(n, H, W, C), self.proj_out, res=x)
+        return ops.conv(h.view(n, H, W, C), self.proj_out, res=x, gn_out=True)
 
 
 class _Motion:
@@ -227,8 +229,9 @@ class _Motion:
         d = C // self.heads
         sc = ops.group_norm(x, self.groups, 1e-6, *self.norm, n)
         lns = torch.empty((rows, 2), dtype=torch.float32, device=x.device)  # LN stats of h, from its GEMM
-        # GN affine materialised (HBM-bound, 2 B/elem each way) so proj_in runs on the DMA GEMM
-        h = ops.conv(ops.group_norm_apply(x, sc[0], sc[1], n, False), self.proj_in, stats_out=lns).view(rows, C)
+        # GN affine folded into the row-block GEMM's A rows (32x32 / 16x16); materialised elsewhere
+        h = ops.conv(x, self.proj_in, aff=(sc[0], sc[1], 1, False), aff_materialize=True,
+                     stats_out=lns).view(rows, C)
         o = torch.empty((rows, C), dtype=torch.bfloat16, device=x.device)
         for a in self.attn:
             pk = a["qkv"]  # LN (+ positional encoding, as the W pe row table) folded in
@@ -241,7 +244,7 @@ class _Motion:
             h = ops.linear(o, a["o"], res=h, stats_out=lns)
         g = ops.linear(h, self.ff1, act=ops.ACT_GEGLU, ln_stats=lns)
         h = ops.linear(g, self.ff2, res=h)
-        return ops.conv(h.view(n, H, W, C), self.proj_out, res=x)
+        return ops.conv(h.view(n, H, W, C), self.proj_out, res=x, gn_out=True)
 
 
 class _DeviceUNet:
@@ -336,7 +339,7 @@ class _DeviceUNet:
     def forward(self, x_in, B, ts_i32, step_i32, audio_rows, n_audio_tok, down_res=None, mid_res=None):
         """x_in NHWC bf16 (B*F, H, W, cin_pad) -> eps NHWC bf16 (B*F, H, W, out_channels)."""
         temb = self.temb(ts_i32, step_i32, B)
-        h = ops.conv(x_in, self.conv_in)
+        h = ops.conv(x_in, self.conv_in, gn_out=True)
         skips = [h]
         for layers, ds in self.down:
             for r, a, m in layers:
@@ -347,7 +350,7 @@ class _DeviceUNet:
                     h = m(h, B)
                 skips.append(h)
             if ds is not None:
-                h = ops.conv(h, ds, stride=2, pad=1)
+                h = ops.conv(h, ds, stride=2, pad=1, gn_out=True)
                 skips.append(h)
         if down_res is not None:
             skips = [s + r for s, r in zip(skips, down_res)]
@@ -367,7 +370,7 @@ class _DeviceUNet:
                 if m is not None:
                     h = m(h, B)
             if us is not None:
-                h = ops.conv(h, us, upsample=True)
+                h = ops.conv(h, us, upsample=True, gn_out=True)
         sc = ops.group_norm(h, self.groups, self.eps, *self.norm_out, B)
         return ops.conv(ops.group_norm_apply(h, sc[0], sc[1], B, True), self.conv_out)
 

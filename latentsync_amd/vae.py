@@ -6,9 +6,11 @@ restatement of its published algorithm (parity against
 the CPU oracle, "parity unpinned" against diffusers itself).  Same public surface
 as diffusers: ``encode(x).latent_dist.sample(generator)``, ``decode(z).sample``,
 ``config.scaling_factor / shift_factor / block_out_channels / latent_channels``,
-``enable_slicing`` / ``disable_slicing``.  Internally NHWC bf16, every GroupNorm
-fused into the next conv's prologue, mid attention on the flash kernel
-(1 head, d = 512).
+``enable_slicing`` / ``disable_slicing``.  Internally NHWC bf16.  GroupNorm:
+statistics from the producing conv's epilogue column sums (ops.conv(gn_out=True)
+-> ls_groupnorm_colsum, no read pass), the affine (+SiLU) materialised once by
+ls_groupnorm_apply -- a 3x3 conv's gather would recompute it for each of its 9
+taps.  Mid attention on the flash kernel (1 head, d = 512).
 """
 import os
 from dataclasses import dataclass
@@ -47,10 +49,10 @@ class _Res:
     def __call__(self, x):
         n = x.shape[0]
         s1 = ops.group_norm(x, 32, 1e-6, *self.n1, n)
-        h = ops.conv(ops.group_norm_apply(x, s1[0], s1[1], n, True), self.c1)
+        h = ops.conv(ops.group_norm_apply(x, s1[0], s1[1], n, True), self.c1, gn_out=True)
         s2 = ops.group_norm(h, 32, 1e-6, *self.n2, n)
         res = x if self.sc is None else ops.conv(x, self.sc)
-        return ops.conv(ops.group_norm_apply(h, s2[0], s2[1], n, True), self.c2, res=res)
+        return ops.conv(ops.group_norm_apply(h, s2[0], s2[1], n, True), self.c2, res=res, gn_out=True)
 
 
 class _Attn:
@@ -70,7 +72,7 @@ class _Attn:
         st = (N * 3 * C, 0, 3 * C, C)
         ops.attention(qkv, qkv[:, C:], qkv[:, 2 * C:], o, batch=n, z2=1, heads=1, nq=N, nk=N, head_dim=C, qs=st,
                       ks=st, vs=st, os_=(N * C, 0, C, C))
-        return ops.linear(o, self.out, res=x.view(n * N, C)).view(n, H, W, C)
+        return ops.conv(o.view(n, H, W, C), self.out, res=x, gn_out=True)
 
 
 class _DeviceVAE:
@@ -104,13 +106,14 @@ class _DeviceVAE:
 
     def encode_moments(self, x):
         """x NHWC bf16 (n, R, R, 8) (3 used channels) -> moments fp32 (n, R/8, R/8, 8)."""
-        h = ops.conv(x, self.enc_in)
+        h = ops.conv(x, self.enc_in, gn_out=True)
         for res, ds in self.enc:
             for r in res:
                 h = r(h)
             if ds is not None:
                 H = h.shape[1]
-                h = ops.conv(h, ds, stride=2, pad=0, out_hw=(H // 2, h.shape[2] // 2))  # F.pad(0,1,0,1) + s2
+                h = ops.conv(h, ds, stride=2, pad=0, out_hw=(H // 2, h.shape[2] // 2),  # F.pad(0,1,0,1) + s2
+                             gn_out=True)
         for blk in self.enc_mid:
             h = blk(h)
         s = ops.group_norm(h, 32, 1e-6, *self.enc_norm, h.shape[0])
@@ -120,14 +123,14 @@ class _DeviceVAE:
     def decode(self, z):
         """z NHWC bf16 (n, h, w, 8) (4 used channels, already / scaling) -> (n, 8h, 8w, 4) bf16."""
         h = ops.conv(z, self.post_quant)
-        h = ops.conv(h, self.dec_in)
+        h = ops.conv(h, self.dec_in, gn_out=True)
         for blk in self.dec_mid:
             h = blk(h)
         for res, us in self.dec:
             for r in res:
                 h = r(h)
             if us is not None:
-                h = ops.conv(h, us, upsample=True)
+                h = ops.conv(h, us, upsample=True, gn_out=True)
         s = ops.group_norm(h, 32, 1e-6, *self.dec_norm, h.shape[0])
         return ops.conv(ops.group_norm_apply(h, s[0], s[1], h.shape[0], True), self.dec_out)
 

@@ -1,6 +1,7 @@
 """Per-kernel parity on MI355X: every C-ABI entry point against a plain
 PyTorch fp32 CPU reference of the same op, on the same bf16-rounded inputs.
 Tolerances are stated per test (bf16 output rounding + fp32 accumulation)."""
+import ctypes
 import math
 
 import pytest
@@ -401,3 +402,81 @@ def test_linear_row_stats_out(gpu, K, M, N, res):
     ref = ops.row_stats(y)
     assert (st[:, 0] - ref[:, 0]).abs().max().item() < 1e-4 * max(1.0, ref[:, 0].abs().max().item())
     assert ((st[:, 1] - ref[:, 1]).abs() / ref[:, 1]).max().item() < 1e-3
+
+
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("case", ["conv3x3_res", "linear_split2", "rowblock_res"])
+def test_gn_colsum(gpu, forced_tile, tile, case):
+    """GroupNorm statistics from the producer (ls_conv_desc.gn_colsum_out): the tile
+    epilogues and the read-pass fallbacks (small tiles, split-K, row-block) against
+    the fp64 sums of the stored bf16 output, and ls_groupnorm_colsum against the
+    read-pass ls_groupnorm on the same tensor (fp64 merge: rel 1e-4)."""
+    if case == "conv3x3_res":
+        n, H, cin, cout, spp = 8, 16, 128, 192, 4
+        x = nhwc(bf(rnd(n, cin, H, H, seed=60)))
+        pw = packed(bf(rnd(cout, cin, 3, 3, seed=61, scale=1 / math.sqrt(9 * cin))), rnd(cout, seed=62) + 3.0, 3)
+        res = nhwc(bf(rnd(n, cout, H, H, seed=63)))
+        forced_tile(tile)
+        y = ops.conv(x, pw, res=res, gn_out=True)
+    else:
+        M, K, N = (1024, 640, 320) if case == "linear_split2" else (512, 320, 320)
+        n, H, spp, cout = M // 64, 8, 4, N
+        x = bf(rnd(M, K, seed=64)).to(torch.bfloat16).to(DEV).view(n, H, H, K)
+        pw = packed(bf(rnd(N, K, seed=65, scale=1 / math.sqrt(K))), rnd(N, seed=66) - 2.0, 1)
+        res = bf(rnd(M, N, seed=67)).to(torch.bfloat16).to(DEV).view(n, H, H, N)
+        forced_tile(tile, 2 if case == "linear_split2" else 0)
+        y = ops.conv(x, pw, res=res, gn_out=True, split_k=2 if case == "linear_split2" else 0)
+    forced_tile(0)
+    cs = y.gn_cs.cpu().double()
+    yf = y.float().cpu().double().reshape(-1, 128, cout)
+    s1, s2 = yf.sum(1), (yf * yf).sum(1)
+    assert (cs[:, 0] - s1).abs().max() <= 1e-5 * yf.abs().sum(1).max()
+    assert (cs[:, 1] - s2).abs().max() <= 1e-5 * s2.max()
+    S = n // spp
+    gamma, beta = (1 + 0.1 * rnd(cout, seed=68)).to(DEV), (0.1 * rnd(cout, seed=69)).to(DEV)
+    sc, sh = ops.group_norm(y, 32, 1e-6, gamma, beta, S)
+    y2 = y.clone()  # no producer sums: the read pass
+    sc2, sh2 = ops.group_norm(y2, 32, 1e-6, gamma, beta, S)
+    assert rel_err(sc.cpu(), sc2.cpu()) < 1e-4 and rel_err(sh.cpu(), sh2.cpu()) < 1e-4
+
+
+def test_groupnorm_colsum_concat(gpu):
+    """Up-block GroupNorm over cat(x, skip): both halves' producer sums, groups
+    straddling the concat boundary (C1 = 96, C2 = 64, 32 groups of 5)."""
+    n, H = 4, 16
+    xa = nhwc(bf(rnd(n, 96, H, H, seed=70) * 2 + 1))
+    xb = nhwc(bf(rnd(n, 64, H, H, seed=71) - 4))
+    ops.gn_colsum(xa)
+    ops.gn_colsum(xb)
+    gamma, beta = (1 + 0.1 * rnd(160, seed=72)).to(DEV), (0.1 * rnd(160, seed=73)).to(DEV)
+    sc, sh = ops.group_norm(xa, 32, 1e-6, gamma, beta, 2, x2=xb)
+    sc2, sh2 = ops.group_norm(xa.clone(), 32, 1e-6, gamma, beta, 2, x2=xb.clone())
+    assert rel_err(sc.cpu(), sc2.cpu()) < 1e-4 and rel_err(sh.cpu(), sh2.cpu()) < 1e-4
+
+
+@pytest.mark.parametrize("K,M,N,H,silu", [(320, 65536, 320, 32, False), (640, 32768, 640, 16, False),
+                                          (320, 65536, 960, 32, True), (1280, 512, 1280, 16, False)])
+def test_gn_affine_fold(gpu, K, M, N, H, silu):
+    """GroupNorm affine (+SiLU) prologue folded into the row-block GEMM's register-resident
+    A rows (ls_conv_path 1 for K = 320 / 640; K = 1280 takes the materialising fallback),
+    against materialise-then-GEMM; with the LayerNorm row statistics of the output
+    (whole rows per block: M >= 256 row blocks, as at the UNet's 32x32 / 16x16 levels)."""
+    from latentsync_amd import _lib
+    n = M // (H * H)  # per-frame GroupNorm: one sample per image
+    x = bf(rnd(M, K, seed=80) * 2 + 1).to(torch.bfloat16).to(DEV).view(n, H, H, K)
+    pw = packed(bf(rnd(N, K, seed=81, scale=1 / math.sqrt(K))), rnd(N, seed=82, scale=0.1), 1)
+    sc = (1 + 0.2 * rnd(n, K, seed=83)).to(DEV)
+    sh = (0.3 * rnd(n, K, seed=84)).to(DEV)
+    st1 = torch.empty((M, 2), dtype=torch.float32, device=DEV)
+    st2 = torch.empty_like(st1)
+    y1 = ops.conv(x, pw, aff=(sc, sh, 1, silu), aff_materialize=True, stats_out=st1)
+    y2 = ops.conv(ops.group_norm_apply(x, sc, sh, n, silu), pw, stats_out=st2)
+    assert rel_err(y1.float().cpu(), y2.float().cpu()) < 1e-2
+    assert rel_err(st1.cpu(), st2.cpu()) < 1e-2
+    # the fold really is the row-block path where it applies
+    d = _lib.ConvDesc()
+    d.x1, d.C1, d.ld1, d.n_img, d.H, d.W, d.Ho, d.Wo, d.ksize, d.stride = x.data_ptr(), K, K, n, H, H, H, H, 1, 1
+    d.aff_scale, d.aff_shift, d.imgs_per_sample = sc.data_ptr(), sh.data_ptr(), 1
+    d.w, d.K, d.N, d.y, d.ldy = pw.w.data_ptr(), pw.K, pw.N, y1.data_ptr(), N
+    d.row_stats_out = st1.data_ptr()
+    assert _lib.load().ls_conv_path(ctypes.byref(d)) == (1 if K in (320, 640) else 2)
