@@ -209,13 +209,13 @@ __device__ __forceinline__ void stage_acc(f32x4 (&acc)[BM / WM / 16][BN / WN / 1
 // slot -- what gn_stats_kernel would read back; ls_groupnorm_colsum merges the slots
 // of a sample in fp64.  The store loop writes the rounded values back over its fp32
 // staging; after the pass barrier one thread per column adds the pass's rows from LDS
-// (2 registers across passes -- the 256x256 kernel is at its VGPR limit), then a
-// barrier before the next pass re-stages.  A slot's sums go out with its last pass.
+// (2 registers across passes), then a barrier before the next pass re-stages.  A
+// slot's sums go out with its last pass.  128-row tiles only (cs_tile_fits).
 constexpr int CS_ROWS = LS_GN_SLOT_ROWS;
 
 template <int BM, int BN, int WM, int WN>
 __host__ __device__ constexpr bool cs_tile_fits() {
-  return BM % CS_ROWS == 0 && CS_ROWS % (BM / WM) == 0 && WM * WN * 64 >= BN;
+  return BM != 256 && BM % CS_ROWS == 0 && CS_ROWS % (BM / WM) == 0 && WM * WN * 64 >= BN;
 }
 
 template <int BM, int BN, int WM, int WN, bool GEN>
@@ -1983,7 +1983,9 @@ extern "C" int ls_conv2d(const ls_conv_desc* d, void* stream) {
   // epilogue column sums: single-pass vectorised epilogue and a tile whose staging
   // buffer holds the per-thread partials (cs_tile_fits; not 128x32 / 64x64)
   const bool vec = (a.N % 8 == 0) && (a.ldy % 8 == 0) && (!a.res || a.ldr % 8 == 0);
-  const bool cs_epi = cs && a.split == 1 && vec && !(t.bm == 128 && t.bn == 32) && t.bm != 64;
+  // (not the 256-row kernels: compiled in, the sums cost their main loop ~12 % -- they run
+  // at the 256-VGPR limit -- against a ~15 us read pass; same-box A/B, scripts/ab_lib.sh)
+  const bool cs_epi = cs && a.split == 1 && vec && !(t.bm == 128 && t.bn == 32) && t.bm != 64 && t.bm < 256;
   if (cs_epi) a.cs_out = cs;
   if (t.bm == 257 && !a.aff_scale && !g_force_regstage && (d->ksize == 1 || tapu)) {  // phased 256x256
     if (d->ksize == 1) launch_p8_1<1, false>(a, grid, s);

@@ -7,6 +7,7 @@ Activations are NHWC bf16: (images, H, W, C) with frames folded into images.
 """
 import ctypes as C
 import math
+import os
 
 import torch
 
@@ -14,6 +15,7 @@ from . import _lib
 from ._lib import check
 
 ACT_NONE, ACT_GEGLU, ACT_GELU, ACT_SILU = 0, 1, 2, 3
+_GN_EPILOGUE = os.environ.get("LS_GN_EPILOGUE", "1") != "0"  # A/B switch: 0 = GroupNorm stats by read pass
 GN_SLOT_ROWS = 128  # LS_GN_SLOT_ROWS
 
 
@@ -132,7 +134,7 @@ def conv(x, pw: Packed, *, x2=None, aff=None, stride=1, pad=None, upsample=False
                     out_scale=out_scale, act=act, out=out, out_f32=out_f32, split_k=split_k, ln_stats=ln_stats,
                     stats_out=stats_out, gn_out=gn_out)
     cs = None
-    if gn_out and (n * Ho * Wo) % GN_SLOT_ROWS == 0 and out.dtype == torch.bfloat16 and act != ACT_GEGLU:
+    if gn_out and _GN_EPILOGUE and (n * Ho * Wo) % GN_SLOT_ROWS == 0 and out.dtype == torch.bfloat16 and act != ACT_GEGLU:
         assert pw.n_out == pw.N
         cs = torch.empty((n * Ho * Wo // GN_SLOT_ROWS, 2, n_out), dtype=torch.float32, device=x.device)
         d.gn_colsum_out = _p(cs)
