@@ -428,19 +428,6 @@ __global__ void __launch_bounds__(256, KC >= 5 ? 1 : 2) attn3_kernel(AttnArgs a)
 // K fragment reads (ds_read_b128, 16 keys x one plane per 16-lane group) are
 // conflict-free; V planes are stored with a rotation of 8 keys per plane so the
 // transposed PV reads (ds_read_b64_tr_b16 over two adjacent planes) are too.
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-__device__ void ls_raw_buffer_load_lds(i32x4 rsrc, __attribute__((address_space(3))) void* lds, int size, int voffset,
-                                       int soffset, int offset, int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
-
-__device__ __forceinline__ i32x4 buffer_rsrc(const void* base, uint32_t bytes) {
-  const unsigned long long b = (unsigned long long)base;
-  i32x4 r;
-  r[0] = (int)(uint32_t)b;
-  r[1] = (int)(uint32_t)(b >> 32);  // stride 0
-  r[2] = (int)bytes;                // num_records (bytes): loads at or past it return 0
-  r[3] = 0x00020000;                // gfx9 raw-buffer dword 3
-  return r;
-}
 
 template <int N>
 __device__ __forceinline__ void attn_wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }

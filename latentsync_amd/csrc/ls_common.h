@@ -8,6 +8,23 @@
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// buffer_load ... lds (LDS-DMA through a buffer descriptor): LDS destination = M0 base
+// + lane * size; the global byte offset = voffset (per lane) + soffset (uniform); a
+// piece whose voffset + soffset reaches num_records reads zeros.
+__device__ void ls_raw_buffer_load_lds(i32x4 rsrc, __attribute__((address_space(3))) void* lds, int size, int voffset,
+                                       int soffset, int offset, int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
+
+__device__ __forceinline__ i32x4 buffer_rsrc(const void* base, uint32_t bytes) {
+  const unsigned long long b = (unsigned long long)base;
+  i32x4 r;
+  r[0] = (int)(uint32_t)b;
+  r[1] = (int)(uint32_t)(b >> 32);  // stride 0
+  r[2] = (int)bytes;                // num_records (bytes): loads at or past it return 0
+  r[3] = 0x00020000;                // gfx9 raw-buffer dword 3
+  return r;
+}
 typedef uint16_t u16;
 
 namespace ls {

@@ -636,7 +636,107 @@ __device__ __forceinline__ int swz_bk(int row, int c) {
   return row * 4 + (c ^ ((-(row >> 2)) & 3));
 }
 
-template <int BM, int BN, int WM, int WN, int KS, bool TAPU, int NST, int BK, int EPI>
+// Operand DMA through buffer descriptors for a BM x BN x 64 tile whose threads each
+// move AI A pieces and BI B pieces of 16 B per K-tile (LDS images lane-linear per
+// wave, 64 pieces per wave-instruction; the XOR swizzle is folded into the chunk
+// offsets ach / bch).  See conv_gemm_dma_kernel's BUF note.
+template <int BM, int BN, int AI, int BI, int KS>
+struct BufDma {
+  static constexpr int CPR = 8;
+  i32x4 rs_a1, rs_a2, rs_b;
+  int avo1[AI], avo2[AI], bvo[BI];
+  unsigned amask[AI];
+  int tap = 0, c0 = 0;  // 3x3: the tap / channel offset of the next K-tile (K-tiles are issued in order)
+
+  __device__ __forceinline__ void init(const ConvArgs& a, int m0, int n0, int wid, int lane, const int* ach,
+                                       const int* bch) {
+    const long cap = 0x7FFFFFFFL;
+    if (KS == 1) {
+      rs_a1 = buffer_rsrc(a.x1 + (long)m0 * a.ld1, (uint32_t)min((long)(a.M - m0) * a.ld1 * 2, cap));
+      rs_a2 = rs_a1;
+#pragma unroll
+      for (int p = 0; p < AI; ++p) {
+        const int row = ((wid * AI + p) * 64 + lane) / CPR;
+        avo1[p] = (row * a.ld1 + ach[p] * 8) * 2;
+        avo2[p] = avo1[p];
+        amask[p] = 0x1FF;
+      }
+    } else {
+      const int HW = a.H * a.W;
+      const long base_pix = (long)(m0 / HW) * HW - a.W - 1;
+      const long tot_pix = (long)a.n_img * HW;
+      rs_a1 = buffer_rsrc(a.x1 + base_pix * a.ld1, (uint32_t)min((tot_pix - base_pix) * a.ld1 * 2, cap));
+      rs_a2 = a.C2 ? buffer_rsrc(a.x2 + base_pix * a.ld2, (uint32_t)min((tot_pix - base_pix) * a.ld2 * 2, cap))
+                   : rs_a1;
+#pragma unroll
+      for (int p = 0; p < AI; ++p) {
+        const int m = m0 + ((wid * AI + p) * 64 + lane) / CPR;
+        const int n = m / HW, r = m - n * HW;
+        const int yo = r / a.W, xo = r - yo * a.W;
+        const int win = (int)((long)n * HW + (long)(yo - 1) * a.W + (xo - 1) - base_pix);
+        avo1[p] = (win * a.ld1 + ach[p] * 8) * 2;
+        avo2[p] = (win * a.ld2 + ach[p] * 8) * 2;
+        unsigned mk = 0;
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) {
+            const bool ok = m < a.M && (unsigned)(yo - 1 + kh) < (unsigned)a.H && (unsigned)(xo - 1 + kw) < (unsigned)a.W;
+            mk |= (ok ? 1u : 0u) << (kh * 3 + kw);
+          }
+        amask[p] = mk;
+      }
+    }
+    rs_b = buffer_rsrc(a.w + (long)n0 * a.K, (uint32_t)min((long)(a.N - n0) * a.K * 2, cap));
+#pragma unroll
+    for (int p = 0; p < BI; ++p) {
+      const int row = ((wid * BI + p) * 64 + lane) / CPR;
+      bvo[p] = (row * a.K + bch[p] * 8) * 2;
+    }
+  }
+
+  // K-tile kt into the A / B images (uint4 pointers of this stage); wid_u wave-uniform.
+  // 3x3: K-tiles must be issued in increasing order from the first one (tap / c0 advance).
+  __device__ __forceinline__ void issue(const ConvArgs& a, int kt, uint4* a_img, uint4* b_img, int wid_u) {
+    int soff = kt * 128;
+    bool two = false;
+    if (KS == 3) {
+      if (c0 == 0 && tap == 0 && kt != 0) {  // first K-tile of a split: locate it
+        tap = (kt * 64) / a.Cin;
+        c0 = kt * 64 - tap * a.Cin;
+      }
+      const int kh = tap / 3, kw = tap - kh * 3;
+      two = c0 >= a.C1;
+      soff = ((kh * a.W + kw) * (two ? a.ld2 : a.ld1) + (two ? c0 - a.C1 : c0)) * 2;
+    }
+#pragma unroll
+    for (int p = 0; p < AI; ++p) {
+      const int vo = KS == 1 ? avo1[p] : (((amask[p] >> tap) & 1u) ? (two ? avo2[p] : avo1[p]) : (int)0x80000000);
+      ls_raw_buffer_load_lds(two ? rs_a2 : rs_a1, (__attribute__((address_space(3))) void*)(a_img + (wid_u * AI + p) * 64),
+                             16, vo, soff, 0, 0);
+    }
+#pragma unroll
+    for (int p = 0; p < BI; ++p)
+      ls_raw_buffer_load_lds(rs_b, (__attribute__((address_space(3))) void*)(b_img + (wid_u * BI + p) * 64), 16, bvo[p],
+                             kt * 128, 0, 0);
+    if (KS == 3) {
+      c0 += 64;
+      if (c0 == a.Cin) { c0 = 0; ++tap; }
+    }
+  }
+};
+
+// BUF: operand DMA through buffer descriptors (host: buf_dma_ok) -- every per-thread
+// byte offset is computed once; a K-tile only changes the uniform soffset (and, for
+// a 3x3 tap, one select per piece between the precomputed window offset and an
+// out-of-range offset that reads zeros), so the K loop carries no 64-bit address
+// arithmetic: ~90-125 VALU per K-tile less than the global_load_lds path, which
+// competes with the MFMAs for vector issue.  1x1: A rows of the tile from a
+// descriptor at row m0 (rows past M read zeros), B rows from one at column n0.
+// 3x3 (stride 1, pad 1, C1 % 64 == 0): the descriptor starts W + 1 pixels before
+// the tile's first image, so every window's top-left pixel has a non-negative
+// offset; the tap's (kh W + kw) pixel shift and channel offset go in soffset.
+template <int BM, int BN, int WM, int WN, int KS, bool TAPU, int NST, int BK, int EPI, bool BUF = false>
 __global__ void __launch_bounds__(WM * WN * 64) conv_gemm_dma_kernel(ConvArgs a) {
   constexpr int NT = WM * WN * 64;                    // 256 (4 waves) or 512 (8 waves, 256-row tiles)
   constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -690,16 +790,24 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_gemm_dma_kernel(ConvArgs a)
     brow[p] = n0 + row;
     bch[p] = swz_bk<BK>(row, q % CPR) - row * CPR;
   }
+  static_assert(!BUF || (BK == 64 && (KS == 1 || TAPU)), "buffer DMA: BK 64, 1x1 or tap-major 3x3");
+  BufDma<BM, BN, AI, BI, KS> bd;  // BUF (dead code otherwise)
+  if constexpr (BUF) bd.init(a, m0, n0, wid, lane, ach, bch);
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
   auto issue = [&](int kt, int stage) {
     uint4* base = lds + stage * STAGE;
+    if constexpr (BUF) {
+      bd.issue(a, kt, base, base + BM * CPR, wid_u);
+    } else {
 #pragma unroll
-    for (int p = 0; p < AI; ++p)
-      glds16(a_src<KS, TAPU, BK>(a, kt, ach[p], arow[p], geo[p]), base + (wid * AI + p) * 64);
+      for (int p = 0; p < AI; ++p)
+        glds16(a_src<KS, TAPU, BK>(a, kt, ach[p], arow[p], geo[p]), base + (wid * AI + p) * 64);
 #pragma unroll
-    for (int p = 0; p < BI; ++p) {
-      const void* src = brow[p] < a.N ? (const void*)(a.w + (long)brow[p] * a.K + kt * BK + bch[p] * 8)
-                                      : (const void*)ls_zero_page;
-      glds16(src, base + BM * CPR + (wid * BI + p) * 64);
+      for (int p = 0; p < BI; ++p) {
+        const void* src = brow[p] < a.N ? (const void*)(a.w + (long)brow[p] * a.K + kt * BK + bch[p] * 8)
+                                        : (const void*)ls_zero_page;
+        glds16(src, base + BM * CPR + (wid * BI + p) * 64);
+      }
     }
   };
 
@@ -778,7 +886,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_gemm_dma_kernel(ConvArgs a)
 // barrier per K-tile; the next tile's DMA is issued right after the barrier so
 // it has a whole K-tile of MFMAs to land.  MFMA runs are bracketed by
 // s_setprio(1) so the co-resident wave's fragment reads interleave.
-template <int BN, int KS, bool TAPU, int EPI>
+template <int BN, int KS, bool TAPU, int EPI, bool BUF = false>
 __global__ void __launch_bounds__(512) conv_gemm_big_kernel(ConvArgs a) {
   constexpr int BM = 256, BK = 64, WM = 2, WN = 4;
   constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -827,8 +935,16 @@ __global__ void __launch_bounds__(512) conv_gemm_big_kernel(ConvArgs a) {
     brow[p] = n0 + row;
     bch[p] = swz_bk<BK>(row, q % CPR) - row * CPR;
   }
+  static_assert(!BUF || KS == 1 || TAPU, "buffer DMA: 1x1 or tap-major 3x3");
+  BufDma<BM, BN, AI, BI, KS> bd;  // BUF (dead code otherwise)
+  if constexpr (BUF) bd.init(a, m0, n0, wid, lane, ach, bch);
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
   auto issue = [&](int kt, int stage) {
     uint4* base = lds + stage * STAGE;
+    if constexpr (BUF) {
+      bd.issue(a, kt, base, base + BM * CPR, wid_u);
+      return;
+    }
 #pragma unroll
     for (int p = 0; p < AI; ++p)
       glds16(a_src<KS, TAPU, BK>(a, kt, ach[p], arow[p], geo[p]), base + (wid * AI + p) * 64);
@@ -907,15 +1023,19 @@ __global__ void __launch_bounds__(512) conv_gemm_big_kernel(ConvArgs a) {
 // 64 x 32 quadrant of the wave tile (16 MFMAs).  A phase issues the fragment
 // reads it needs (A quadrant rows and/or B quadrant cols), ONE half-tile of
 // operand DMA (2 glds per thread; half-tiles A0 A1 B0 B1 = 128 rows x 64 k)
-// six half-tiles ahead, barrier, MFMAs at raised priority, barrier.  The DMA
-// for tile t+1 is retired by a counted vmcnt(4) in phase 3 of tile t, so
-// operand loads span barriers and never drain in the main loop.
+// D = 5 half-tiles ahead, barrier, waits for its reads (they overlap the
+// barrier), MFMAs at raised priority, barrier.  The DMA for tile t+1 is retired
+// by a counted vmcnt(2) in phase 3 of tile t, so operand loads span barriers and
+// never drain in the main loop.  Hazards (g = 4t + phase): half g+5 overwrites
+// half g-3 -- A0(t) last read by row 0 at 4t+2, re-staged at 4t+3 after that
+// row retired the reads in its own phase 4t+2; A1 at 4t+4, B0 at 4t+5, B1 at
+// 4t+6 (B last read at 4t+1).  Row 1 runs one barrier behind row 0.
 template <int KS, bool TAPU>
 __global__ void __launch_bounds__(512) conv_gemm_p8_kernel(ConvArgs a) {
   constexpr int BM = 256, BN = 256, BK = 64, CPR = 8;
   constexpr int HALF = 128 * CPR;         // uint4 per half-tile (16 KB)
   constexpr int BUF = 4 * HALF;           // A0 A1 B0 B1
-  constexpr int D = 6;                    // half-tiles of DMA in flight
+  constexpr int D = 5;                    // half-tiles of DMA issued ahead
   extern __shared__ __attribute__((aligned(16))) uint4 lds_dyn[];
   uint4* lds = lds_dyn;
 
@@ -990,7 +1110,7 @@ __global__ void __launch_bounds__(512) conv_gemm_p8_kernel(ConvArgs a) {
   // prologue: half-tiles 0 .. D-1 in flight, tile 0 landed
 #pragma unroll
   for (int s = 0; s < D; ++s) issue_half(s);
-  if (nk > 1) wait_vm<4>(); else wait_vm<0>();
+  if (nhalf > 4) wait_vm<2>(); else wait_vm<0>();  // tile 0 (halves 0..3) landed, half 4 in flight
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 
@@ -1037,15 +1157,12 @@ __global__ void __launch_bounds__(512) conv_gemm_p8_kernel(ConvArgs a) {
       (void)arow_w;
       // one half-tile of DMA, D ahead
       issue_half(4 * t + ph + D);
-      if (ph == 3) {  // retire tile t+1 (issued up to 4t+9 now; t+1 ends at 4t+7)
-        if (4 * t + 3 + D < nhalf) wait_vm<4>();
+      if (ph == 3) {  // retire tile t+1 (issued up to 4t+8 now; t+1 ends at 4t+7)
+        if (4 * t + 3 + D < nhalf) wait_vm<2>();
         else wait_vm<0>();
       }
-      // this phase's fragment reads retire before the barrier: a half-tile may be
-      // re-staged by the other wave row right after it
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this phase's reads, overlapped with the barrier
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
@@ -1754,23 +1871,44 @@ static int epi_kind(const ConvArgs& a) {
   return EPI_ANY;
 }
 
-template <int BM, int BN, int WM, int WN, int KS, bool TAPU, int NST, int BK, int EPI>
+template <int BM, int BN, int WM, int WN, int KS, bool TAPU, int NST, int BK, int EPI, bool BUF = false>
 static void launch_dma1(const ConvArgs& a, int grid, hipStream_t s) {
   // staging for the epilogue must fit too
   const size_t shm = std::max<size_t>((size_t)NST * (BM + BN) * (BK / 8) * 16, (size_t)(BM / WM) * (BN + 4) * 4);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_gemm_dma_kernel<BM, BN, WM, WN, KS, TAPU, NST, BK, EPI>,
+    (void)hipFuncSetAttribute((const void*)conv_gemm_dma_kernel<BM, BN, WM, WN, KS, TAPU, NST, BK, EPI, BUF>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     attr = true;
   }
-  conv_gemm_dma_kernel<BM, BN, WM, WN, KS, TAPU, NST, BK, EPI><<<grid, WM * WN * 64, shm, s>>>(a);
+  conv_gemm_dma_kernel<BM, BN, WM, WN, KS, TAPU, NST, BK, EPI, BUF><<<grid, WM * WN * 64, shm, s>>>(a);
+}
+
+static bool g_no_buf_dma = getenv("LS_GEMM_GLDS") != nullptr;  // A/B switch: global_load_lds addressing
+
+// operand DMA through buffer descriptors: 1x1 with one source and K == Cin % 64 == 0;
+// tap-major 3x3, stride 1, pad 1, no upsample, C1 % 64 == 0 (a K-tile never straddles
+// the concat); byte offsets of a tile's window must fit 31 bits (they do: < 16 MB)
+static bool buf_dma_ok(const ConvArgs& a, int ks) {
+  if (g_no_buf_dma || a.aff_scale) return false;
+  if (ks == 1) return a.C2 == 0 && a.Cin % 64 == 0 && a.K == a.Cin;
+  return a.Cin % 64 == 0 && a.C1 % 64 == 0 && a.stride == 1 && !a.upsample && a.pad == 1 && a.Ho == a.H &&
+         a.Wo == a.W;
 }
 
 template <int BM, int BN, int WM, int WN, int KS, bool TAPU>
 static void launch_dma(const ConvArgs& a, int grid, hipStream_t s) {
   if constexpr (BN >= 64) {
     if (g_bk == 32) { launch_dma1<BM, BN, WM, WN, KS, TAPU, 4, 32, EPI_ANY>(a, grid, s); return; }
+  }
+  if constexpr (KS == 1 || TAPU) {
+    if (buf_dma_ok(a, KS)) {
+      switch (epi_kind(a)) {
+        case EPI_PLAIN: launch_dma1<BM, BN, WM, WN, KS, TAPU, 2, 64, EPI_PLAIN, true>(a, grid, s); return;
+        case EPI_GEGLU: launch_dma1<BM, BN, WM, WN, KS, TAPU, 2, 64, EPI_GEGLU, true>(a, grid, s); return;
+        default: launch_dma1<BM, BN, WM, WN, KS, TAPU, 2, 64, EPI_ANY, true>(a, grid, s); return;
+      }
+    }
   }
   switch (epi_kind(a)) {
     case EPI_PLAIN: launch_dma1<BM, BN, WM, WN, KS, TAPU, 2, 64, EPI_PLAIN>(a, grid, s); break;
@@ -1779,20 +1917,29 @@ static void launch_dma(const ConvArgs& a, int grid, hipStream_t s) {
   }
 }
 
-template <int BN, int KS, bool TAPU, int EPI>
+template <int BN, int KS, bool TAPU, int EPI, bool BUF = false>
 static void launch_big2(const ConvArgs& a, int grid, hipStream_t s) {
   const size_t shm = std::max<size_t>((size_t)2 * (256 + BN) * 8 * 16, (size_t)128 * (BN + 4) * 4);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_gemm_big_kernel<BN, KS, TAPU, EPI>,
+    (void)hipFuncSetAttribute((const void*)conv_gemm_big_kernel<BN, KS, TAPU, EPI, BUF>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     attr = true;
   }
-  conv_gemm_big_kernel<BN, KS, TAPU, EPI><<<grid, 512, shm, s>>>(a);
+  conv_gemm_big_kernel<BN, KS, TAPU, EPI, BUF><<<grid, 512, shm, s>>>(a);
 }
 
 template <int BN, int KS, bool TAPU>
 static void launch_big1(const ConvArgs& a, int grid, hipStream_t s) {
+  if constexpr (KS == 1 || TAPU) {
+    if (buf_dma_ok(a, KS)) {
+      switch (epi_kind(a)) {
+        case EPI_PLAIN: launch_big2<BN, KS, TAPU, EPI_PLAIN, true>(a, grid, s); return;
+        case EPI_GEGLU: launch_big2<BN, KS, TAPU, EPI_GEGLU, true>(a, grid, s); return;
+        default: launch_big2<BN, KS, TAPU, EPI_ANY, true>(a, grid, s); return;
+      }
+    }
+  }
   switch (epi_kind(a)) {
     case EPI_PLAIN: launch_big2<BN, KS, TAPU, EPI_PLAIN>(a, grid, s); break;
     case EPI_GEGLU: launch_big2<BN, KS, TAPU, EPI_GEGLU>(a, grid, s); break;
