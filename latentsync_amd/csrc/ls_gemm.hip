@@ -651,29 +651,30 @@ struct BufDma {
   __device__ __forceinline__ void init(const ConvArgs& a, int m0, int n0, int wid, int lane, const int* ach,
                                        const int* bch) {
     const long cap = 0x7FFFFFFFL;
-    if (KS == 1) {
+    if (KS == 1) {  // (rows of one tile: the concat halves share the row index)
       rs_a1 = buffer_rsrc(a.x1 + (long)m0 * a.ld1, (uint32_t)min((long)(a.M - m0) * a.ld1 * 2, cap));
-      rs_a2 = rs_a1;
+      rs_a2 = a.C2 ? buffer_rsrc(a.x2 + (long)m0 * a.ld2, (uint32_t)min((long)(a.M - m0) * a.ld2 * 2, cap)) : rs_a1;
 #pragma unroll
       for (int p = 0; p < AI; ++p) {
         const int row = ((wid * AI + p) * 64 + lane) / CPR;
         avo1[p] = (row * a.ld1 + ach[p] * 8) * 2;
-        avo2[p] = avo1[p];
+        avo2[p] = (row * a.ld2 + ach[p] * 8) * 2;
         amask[p] = 0x1FF;
       }
-    } else {
-      const int HW = a.H * a.W;
-      const long base_pix = (long)(m0 / HW) * HW - a.W - 1;
-      const long tot_pix = (long)a.n_img * HW;
+    } else {  // output pixel (yo, xo) reads input (yo s - pad + kh, xo s - pad + kw)
+      const int HWi = a.H * a.W, HWo = a.Ho * a.Wo;
+      const long base_pix = (long)(m0 / HWo) * HWi - (long)a.pad * a.W - a.pad;
+      const long tot_pix = (long)a.n_img * HWi;
       rs_a1 = buffer_rsrc(a.x1 + base_pix * a.ld1, (uint32_t)min((tot_pix - base_pix) * a.ld1 * 2, cap));
       rs_a2 = a.C2 ? buffer_rsrc(a.x2 + base_pix * a.ld2, (uint32_t)min((tot_pix - base_pix) * a.ld2 * 2, cap))
                    : rs_a1;
 #pragma unroll
       for (int p = 0; p < AI; ++p) {
         const int m = m0 + ((wid * AI + p) * 64 + lane) / CPR;
-        const int n = m / HW, r = m - n * HW;
-        const int yo = r / a.W, xo = r - yo * a.W;
-        const int win = (int)((long)n * HW + (long)(yo - 1) * a.W + (xo - 1) - base_pix);
+        const int n = m / HWo, r = m - n * HWo;
+        const int yo = r / a.Wo, xo = r - yo * a.Wo;
+        const int yt = yo * a.stride - a.pad, xt = xo * a.stride - a.pad;  // window top-left
+        const int win = (int)((long)n * HWi + (long)yt * a.W + xt - base_pix);
         avo1[p] = (win * a.ld1 + ach[p] * 8) * 2;
         avo2[p] = (win * a.ld2 + ach[p] * 8) * 2;
         unsigned mk = 0;
@@ -681,7 +682,7 @@ struct BufDma {
         for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
           for (int kw = 0; kw < 3; ++kw) {
-            const bool ok = m < a.M && (unsigned)(yo - 1 + kh) < (unsigned)a.H && (unsigned)(xo - 1 + kw) < (unsigned)a.W;
+            const bool ok = m < a.M && (unsigned)(yt + kh) < (unsigned)a.H && (unsigned)(xt + kw) < (unsigned)a.W;
             mk |= (ok ? 1u : 0u) << (kh * 3 + kw);
           }
         amask[p] = mk;
@@ -700,6 +701,10 @@ struct BufDma {
   __device__ __forceinline__ void issue(const ConvArgs& a, int kt, uint4* a_img, uint4* b_img, int wid_u) {
     int soff = kt * 128;
     bool two = false;
+    if (KS == 1 && a.C2) {  // concat: a K-tile lies in one source (host: C1 % 64 == 0)
+      two = kt * 64 >= a.C1;
+      soff = two ? (kt * 64 - a.C1) * 2 : soff;
+    }
     if (KS == 3) {
       if (c0 == 0 && tap == 0 && kt != 0) {  // first K-tile of a split: locate it
         tap = (kt * 64) / a.Cin;
@@ -711,7 +716,8 @@ struct BufDma {
     }
 #pragma unroll
     for (int p = 0; p < AI; ++p) {
-      const int vo = KS == 1 ? avo1[p] : (((amask[p] >> tap) & 1u) ? (two ? avo2[p] : avo1[p]) : (int)0x80000000);
+      const int vo = KS == 1 ? (two ? avo2[p] : avo1[p])
+                             : (((amask[p] >> tap) & 1u) ? (two ? avo2[p] : avo1[p]) : (int)0x80000000);
       ls_raw_buffer_load_lds(two ? rs_a2 : rs_a1, (__attribute__((address_space(3))) void*)(a_img + (wid_u * AI + p) * 64),
                              16, vo, soff, 0, 0);
     }
@@ -733,9 +739,10 @@ struct BufDma {
 // arithmetic: ~90-125 VALU per K-tile less than the global_load_lds path, which
 // competes with the MFMAs for vector issue.  1x1: A rows of the tile from a
 // descriptor at row m0 (rows past M read zeros), B rows from one at column n0.
-// 3x3 (stride 1, pad 1, C1 % 64 == 0): the descriptor starts W + 1 pixels before
-// the tile's first image, so every window's top-left pixel has a non-negative
-// offset; the tap's (kh W + kw) pixel shift and channel offset go in soffset.
+// 3x3 (stride 1 / 2, pad 0 / 1, C1 % 64 == 0): the descriptor starts pad (W + 1)
+// pixels before the tile's first input image, so every window's top-left pixel has
+// a non-negative offset; the tap's (kh W + kw) pixel shift and channel offset go in
+// soffset, taps outside the image select an offset past the descriptor (zeros).
 template <int BM, int BN, int WM, int WN, int KS, bool TAPU, int NST, int BK, int EPI, bool BUF = false>
 __global__ void __launch_bounds__(WM * WN * 64) conv_gemm_dma_kernel(ConvArgs a) {
   constexpr int NT = WM * WN * 64;                    // 256 (4 waves) or 512 (8 waves, 256-row tiles)
@@ -1886,14 +1893,15 @@ static void launch_dma1(const ConvArgs& a, int grid, hipStream_t s) {
 
 static bool g_no_buf_dma = getenv("LS_GEMM_GLDS") != nullptr;  // A/B switch: global_load_lds addressing
 
-// operand DMA through buffer descriptors: 1x1 with one source and K == Cin % 64 == 0;
-// tap-major 3x3, stride 1, pad 1, no upsample, C1 % 64 == 0 (a K-tile never straddles
-// the concat); byte offsets of a tile's window must fit 31 bits (they do: < 16 MB)
+// operand DMA through buffer descriptors: 1x1 with K == Cin, Cin % 64 == 0; tap-major 3x3,
+// stride 1 or 2, pad 0 or 1, no upsample; C1 % 64 == 0 (a K-tile never straddles the
+// concat); byte offsets of a tile's window must fit 31 bits (they do: < 16 MB)
 static bool buf_dma_ok(const ConvArgs& a, int ks) {
   if (g_no_buf_dma || a.aff_scale) return false;
-  if (ks == 1) return a.C2 == 0 && a.Cin % 64 == 0 && a.K == a.Cin;
-  return a.Cin % 64 == 0 && a.C1 % 64 == 0 && a.stride == 1 && !a.upsample && a.pad == 1 && a.Ho == a.H &&
-         a.Wo == a.W;
+  if (ks == 1) return a.Cin % 64 == 0 && a.C1 % 64 == 0 && a.K == a.Cin;
+  // (nearest-x2 upsampling gathers are not a fixed shift per tap: global_load_lds path)
+  return a.Cin % 64 == 0 && a.C1 % 64 == 0 && (a.stride == 1 || a.stride == 2) && !a.upsample &&
+         (a.pad == 0 || a.pad == 1);
 }
 
 template <int BM, int BN, int WM, int WN, int KS, bool TAPU>
