@@ -642,23 +642,22 @@ __device__ __forceinline__ int swz_bk(int row, int c) {
 // offsets ach / bch).  See conv_gemm_dma_kernel's BUF note.
 template <int BM, int BN, int AI, int BI, int KS>
 struct BufDma {
-  static constexpr int CPR = 8;
   i32x4 rs_a1, rs_a2, rs_b;
   int avo1[AI], avo2[AI], bvo[BI];
   unsigned amask[AI];
-  int tap = 0, c0 = 0;  // 3x3: the tap / channel offset of the next K-tile (K-tiles are issued in order)
+  int tap = 0, c0 = 0;  // 3x3: tap / channel offset of the next K-tile (next())
 
-  __device__ __forceinline__ void init(const ConvArgs& a, int m0, int n0, int wid, int lane, const int* ach,
-                                       const int* bch) {
+  // arow / brow: tile-relative row of each piece; ach / bch: its logical 16-B chunk
+  __device__ __forceinline__ void init(const ConvArgs& a, int m0, int n0, const int* arow, const int* ach,
+                                       const int* brow, const int* bch) {
     const long cap = 0x7FFFFFFFL;
     if (KS == 1) {  // (rows of one tile: the concat halves share the row index)
       rs_a1 = buffer_rsrc(a.x1 + (long)m0 * a.ld1, (uint32_t)min((long)(a.M - m0) * a.ld1 * 2, cap));
       rs_a2 = a.C2 ? buffer_rsrc(a.x2 + (long)m0 * a.ld2, (uint32_t)min((long)(a.M - m0) * a.ld2 * 2, cap)) : rs_a1;
 #pragma unroll
       for (int p = 0; p < AI; ++p) {
-        const int row = ((wid * AI + p) * 64 + lane) / CPR;
-        avo1[p] = (row * a.ld1 + ach[p] * 8) * 2;
-        avo2[p] = (row * a.ld2 + ach[p] * 8) * 2;
+        avo1[p] = (arow[p] * a.ld1 + ach[p] * 8) * 2;
+        avo2[p] = (arow[p] * a.ld2 + ach[p] * 8) * 2;
         amask[p] = 0x1FF;
       }
     } else {  // output pixel (yo, xo) reads input (yo s - pad + kh, xo s - pad + kw)
@@ -670,7 +669,7 @@ struct BufDma {
                    : rs_a1;
 #pragma unroll
       for (int p = 0; p < AI; ++p) {
-        const int m = m0 + ((wid * AI + p) * 64 + lane) / CPR;
+        const int m = m0 + arow[p];
         const int n = m / HWo, r = m - n * HWo;
         const int yo = r / a.Wo, xo = r - yo * a.Wo;
         const int yt = yo * a.stride - a.pad, xt = xo * a.stride - a.pad;  // window top-left
@@ -690,45 +689,50 @@ struct BufDma {
     }
     rs_b = buffer_rsrc(a.w + (long)n0 * a.K, (uint32_t)min((long)(a.N - n0) * a.K * 2, cap));
 #pragma unroll
-    for (int p = 0; p < BI; ++p) {
-      const int row = ((wid * BI + p) * 64 + lane) / CPR;
-      bvo[p] = (row * a.K + bch[p] * 8) * 2;
-    }
+    for (int p = 0; p < BI; ++p) bvo[p] = (brow[p] * a.K + bch[p] * 8) * 2;
   }
 
-  // K-tile kt into the A / B images (uint4 pointers of this stage); wid_u wave-uniform.
-  // 3x3: K-tiles must be issued in increasing order from the first one (tap / c0 advance).
-  __device__ __forceinline__ void issue(const ConvArgs& a, int kt, uint4* a_img, uint4* b_img, int wid_u) {
-    int soff = kt * 128;
-    bool two = false;
-    if (KS == 1 && a.C2) {  // concat: a K-tile lies in one source (host: C1 % 64 == 0)
-      two = kt * 64 >= a.C1;
-      soff = two ? (kt * 64 - a.C1) * 2 : soff;
-    }
-    if (KS == 3) {
-      if (c0 == 0 && tap == 0 && kt != 0) {  // first K-tile of a split: locate it
+  // uniform per-K-tile offsets.  next(): K-tiles requested in increasing order from the
+  // first (3x3: the tap / channel offset advance; the first of a split divides once)
+  struct KTile { int soff_a, soff_b, tap; bool two; };
+  __device__ __forceinline__ KTile next(const ConvArgs& a, int kt) {
+    KTile k;
+    k.soff_b = kt * 128;
+    if (KS == 1) {
+      k.tap = 0;
+      k.two = a.C2 && kt * 64 >= a.C1;  // concat: a K-tile lies in one source (host: C1 % 64 == 0)
+      k.soff_a = k.two ? (kt * 64 - a.C1) * 2 : kt * 128;
+    } else {
+      if (c0 == 0 && tap == 0 && kt != 0) {
         tap = (kt * 64) / a.Cin;
         c0 = kt * 64 - tap * a.Cin;
       }
       const int kh = tap / 3, kw = tap - kh * 3;
-      two = c0 >= a.C1;
-      soff = ((kh * a.W + kw) * (two ? a.ld2 : a.ld1) + (two ? c0 - a.C1 : c0)) * 2;
-    }
-#pragma unroll
-    for (int p = 0; p < AI; ++p) {
-      const int vo = KS == 1 ? (two ? avo2[p] : avo1[p])
-                             : (((amask[p] >> tap) & 1u) ? (two ? avo2[p] : avo1[p]) : (int)0x80000000);
-      ls_raw_buffer_load_lds(two ? rs_a2 : rs_a1, (__attribute__((address_space(3))) void*)(a_img + (wid_u * AI + p) * 64),
-                             16, vo, soff, 0, 0);
-    }
-#pragma unroll
-    for (int p = 0; p < BI; ++p)
-      ls_raw_buffer_load_lds(rs_b, (__attribute__((address_space(3))) void*)(b_img + (wid_u * BI + p) * 64), 16, bvo[p],
-                             kt * 128, 0, 0);
-    if (KS == 3) {
+      k.tap = tap;
+      k.two = c0 >= a.C1;
+      k.soff_a = ((kh * a.W + kw) * (k.two ? a.ld2 : a.ld1) + (k.two ? c0 - a.C1 : c0)) * 2;
       c0 += 64;
       if (c0 == a.Cin) { c0 = 0; ++tap; }
     }
+    return k;
+  }
+
+  __device__ __forceinline__ void load_a(int p, uint4* dst, const KTile& k) const {
+    const int vo = KS == 1 ? (k.two ? avo2[p] : avo1[p])
+                           : (((amask[p] >> k.tap) & 1u) ? (k.two ? avo2[p] : avo1[p]) : (int)0x80000000);
+    ls_raw_buffer_load_lds(k.two ? rs_a2 : rs_a1, (__attribute__((address_space(3))) void*)dst, 16, vo, k.soff_a, 0, 0);
+  }
+  __device__ __forceinline__ void load_b(int p, uint4* dst, const KTile& k) const {
+    ls_raw_buffer_load_lds(rs_b, (__attribute__((address_space(3))) void*)dst, 16, bvo[p], k.soff_b, 0, 0);
+  }
+
+  // the whole K-tile kt into the A / B images of a stage (pieces lane-linear per wave)
+  __device__ __forceinline__ void issue(const ConvArgs& a, int kt, uint4* a_img, uint4* b_img, int wid_u) {
+    const KTile k = next(a, kt);
+#pragma unroll
+    for (int p = 0; p < AI; ++p) load_a(p, a_img + (wid_u * AI + p) * 64, k);
+#pragma unroll
+    for (int p = 0; p < BI; ++p) load_b(p, b_img + (wid_u * BI + p) * 64, k);
   }
 };
 
@@ -799,7 +803,14 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_gemm_dma_kernel(ConvArgs a)
   }
   static_assert(!BUF || (BK == 64 && (KS == 1 || TAPU)), "buffer DMA: BK 64, 1x1 or tap-major 3x3");
   BufDma<BM, BN, AI, BI, KS> bd;  // BUF (dead code otherwise)
-  if constexpr (BUF) bd.init(a, m0, n0, wid, lane, ach, bch);
+  if constexpr (BUF) {
+    int ar[AI], br[BI];
+#pragma unroll
+    for (int p = 0; p < AI; ++p) ar[p] = arow[p] - m0;
+#pragma unroll
+    for (int p = 0; p < BI; ++p) br[p] = brow[p] - n0;
+    bd.init(a, m0, n0, ar, ach, br, bch);
+  }
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);
   auto issue = [&](int kt, int stage) {
     uint4* base = lds + stage * STAGE;
@@ -944,7 +955,14 @@ __global__ void __launch_bounds__(512) conv_gemm_big_kernel(ConvArgs a) {
   }
   static_assert(!BUF || KS == 1 || TAPU, "buffer DMA: 1x1 or tap-major 3x3");
   BufDma<BM, BN, AI, BI, KS> bd;  // BUF (dead code otherwise)
-  if constexpr (BUF) bd.init(a, m0, n0, wid, lane, ach, bch);
+  if constexpr (BUF) {
+    int ar[AI], br[BI];
+#pragma unroll
+    for (int p = 0; p < AI; ++p) ar[p] = arow[p] - m0;
+#pragma unroll
+    for (int p = 0; p < BI; ++p) br[p] = brow[p] - n0;
+    bd.init(a, m0, n0, ar, ach, br, bch);
+  }
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);
   auto issue = [&](int kt, int stage) {
     uint4* base = lds + stage * STAGE;
