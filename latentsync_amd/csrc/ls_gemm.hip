@@ -660,6 +660,35 @@ struct BufDma {
         avo2[p] = (arow[p] * a.ld2 + ach[p] * 8) * 2;
         amask[p] = 0x1FF;
       }
+    } else if (a.upsample) {
+      // nearest x2 then 3x3 pad 1: upsampled (yo - 1 + kh, xo - 1 + kw) reads input
+      // (i - 1 + r, j - 1 + c), i = yo >> 1, r = (py + kh + 1) >> 1 (py = yo & 1), likewise
+      // c: the tap's uniform shift r0 W + c0 (py = px = 0) plus W / 1 pixel for the odd
+      // rows / columns of taps kh / kw != 1 (parity bits 9 / 10 of amask)
+      const int HWi = a.H * a.W, HWo = a.Ho * a.Wo;
+      const long base_pix = (long)(m0 / HWo) * HWi - a.W - 1;
+      const long tot_pix = (long)a.n_img * HWi;
+      rs_a1 = buffer_rsrc(a.x1 + base_pix * a.ld1, (uint32_t)min((tot_pix - base_pix) * a.ld1 * 2, cap));
+      rs_a2 = a.C2 ? buffer_rsrc(a.x2 + base_pix * a.ld2, (uint32_t)min((tot_pix - base_pix) * a.ld2 * 2, cap))
+                   : rs_a1;
+#pragma unroll
+      for (int p = 0; p < AI; ++p) {
+        const int m = m0 + arow[p];
+        const int n = m / HWo, r = m - n * HWo;
+        const int yo = r / a.Wo, xo = r - yo * a.Wo;
+        const int win = (int)((long)n * HWi + (long)((yo >> 1) - 1) * a.W + ((xo >> 1) - 1) - base_pix);
+        avo1[p] = (win * a.ld1 + ach[p] * 8) * 2;
+        avo2[p] = (win * a.ld2 + ach[p] * 8) * 2;
+        unsigned mk = ((unsigned)(yo & 1) << 9) | ((unsigned)(xo & 1) << 10);
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) {
+            const bool ok = m < a.M && (unsigned)(yo - 1 + kh) < (unsigned)a.Ho && (unsigned)(xo - 1 + kw) < (unsigned)a.Wo;
+            mk |= (ok ? 1u : 0u) << (kh * 3 + kw);
+          }
+        amask[p] = mk;
+      }
     } else {  // output pixel (yo, xo) reads input (yo s - pad + kh, xo s - pad + kw)
       const int HWi = a.H * a.W, HWo = a.Ho * a.Wo;
       const long base_pix = (long)(m0 / HWo) * HWi - (long)a.pad * a.W - a.pad;
@@ -694,10 +723,12 @@ struct BufDma {
 
   // uniform per-K-tile offsets.  next(): K-tiles requested in increasing order from the
   // first (3x3: the tap / channel offset advance; the first of a split divides once)
-  struct KTile { int soff_a, soff_b, tap; bool two; };
+  struct KTile { int soff_a, soff_b, tap, dy, dx; bool two; };
   __device__ __forceinline__ KTile next(const ConvArgs& a, int kt) {
     KTile k;
     k.soff_b = kt * 128;
+    k.dy = 0;
+    k.dx = 0;
     if (KS == 1) {
       k.tap = 0;
       k.two = a.C2 && kt * 64 >= a.C1;  // concat: a K-tile lies in one source (host: C1 % 64 == 0)
@@ -710,16 +741,24 @@ struct BufDma {
       const int kh = tap / 3, kw = tap - kh * 3;
       k.tap = tap;
       k.two = c0 >= a.C1;
-      k.soff_a = ((kh * a.W + kw) * (k.two ? a.ld2 : a.ld1) + (k.two ? c0 - a.C1 : c0)) * 2;
+      const int ld = k.two ? a.ld2 : a.ld1;
+      if (a.upsample) {
+        k.soff_a = ((((kh + 1) >> 1) * a.W + ((kw + 1) >> 1)) * ld + (k.two ? c0 - a.C1 : c0)) * 2;
+        k.dy = kh != 1 ? a.W * ld * 2 : 0;
+        k.dx = kw != 1 ? ld * 2 : 0;
+      } else {
+        k.soff_a = ((kh * a.W + kw) * ld + (k.two ? c0 - a.C1 : c0)) * 2;
+      }
       c0 += 64;
       if (c0 == a.Cin) { c0 = 0; ++tap; }
     }
     return k;
   }
 
-  __device__ __forceinline__ void load_a(int p, uint4* dst, const KTile& k) const {
-    const int vo = KS == 1 ? (k.two ? avo2[p] : avo1[p])
-                           : (((amask[p] >> k.tap) & 1u) ? (k.two ? avo2[p] : avo1[p]) : (int)0x80000000);
+  __device__ __forceinline__ void load_a(int p, uint4* dst, const KTile& k, bool ups = false) const {
+    int v = k.two ? avo2[p] : avo1[p];
+    if (KS == 3 && ups) v += ((amask[p] >> 9) & 1u ? k.dy : 0) + ((amask[p] >> 10) & 1u ? k.dx : 0);
+    const int vo = KS == 1 ? v : (((amask[p] >> k.tap) & 1u) ? v : (int)0x80000000);
     ls_raw_buffer_load_lds(k.two ? rs_a2 : rs_a1, (__attribute__((address_space(3))) void*)dst, 16, vo, k.soff_a, 0, 0);
   }
   __device__ __forceinline__ void load_b(int p, uint4* dst, const KTile& k) const {
@@ -729,8 +768,13 @@ struct BufDma {
   // the whole K-tile kt into the A / B images of a stage (pieces lane-linear per wave)
   __device__ __forceinline__ void issue(const ConvArgs& a, int kt, uint4* a_img, uint4* b_img, int wid_u) {
     const KTile k = next(a, kt);
+    if (KS == 3 && a.upsample) {  // (uniform branch: the parity adds only where they apply)
 #pragma unroll
-    for (int p = 0; p < AI; ++p) load_a(p, a_img + (wid_u * AI + p) * 64, k);
+      for (int p = 0; p < AI; ++p) load_a(p, a_img + (wid_u * AI + p) * 64, k, true);
+    } else {
+#pragma unroll
+      for (int p = 0; p < AI; ++p) load_a(p, a_img + (wid_u * AI + p) * 64, k);
+    }
 #pragma unroll
     for (int p = 0; p < BI; ++p) load_b(p, b_img + (wid_u * BI + p) * 64, k);
   }
@@ -1910,16 +1954,16 @@ static void launch_dma1(const ConvArgs& a, int grid, hipStream_t s) {
 }
 
 static bool g_no_buf_dma = getenv("LS_GEMM_GLDS") != nullptr;  // A/B switch: global_load_lds addressing
+static bool g_no_buf_ups = getenv("LS_GEMM_UPS_GLDS") != nullptr;  // A/B switch: ... for upsampling convs only
 
 // operand DMA through buffer descriptors: 1x1 with K == Cin, Cin % 64 == 0; tap-major 3x3,
-// stride 1 or 2, pad 0 or 1, no upsample; C1 % 64 == 0 (a K-tile never straddles the
+// stride 1 or 2, pad 0 or 1, or nearest-x2 upsample with pad 1; C1 % 64 == 0 (a K-tile never straddles the
 // concat); byte offsets of a tile's window must fit 31 bits (they do: < 16 MB)
 static bool buf_dma_ok(const ConvArgs& a, int ks) {
   if (g_no_buf_dma || a.aff_scale) return false;
   if (ks == 1) return a.Cin % 64 == 0 && a.C1 % 64 == 0 && a.K == a.Cin;
-  // (nearest-x2 upsampling gathers are not a fixed shift per tap: global_load_lds path)
-  return a.Cin % 64 == 0 && a.C1 % 64 == 0 && (a.stride == 1 || a.stride == 2) && !a.upsample &&
-         (a.pad == 0 || a.pad == 1);
+  if (a.upsample) return !g_no_buf_ups && a.Cin % 64 == 0 && a.C1 % 64 == 0 && a.stride == 1 && a.pad == 1;
+  return a.Cin % 64 == 0 && a.C1 % 64 == 0 && (a.stride == 1 || a.stride == 2) && (a.pad == 0 || a.pad == 1);
 }
 
 template <int BM, int BN, int WM, int WN, int KS, bool TAPU>
