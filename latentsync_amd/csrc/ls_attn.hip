@@ -12,7 +12,8 @@
 // and V^T comes from the row-major V tile through ds_read_b64_tr_b16.
 //
 // Kernels (dispatch in ls_attention):
-//   attn_seq_kernel  short sequences (the temporal attention over a window's frames)
+//   attn_seqm_kernel short sequences (the temporal attention over a window's frames), MFMA
+//   attn_seq_kernel  the same with packed-bf16 dot products (d = 160, A/B baseline)
 //   attn5_kernel     d = 40 self attention: DMA-fed K/V planes, 64 queries per wave
 //   attn3_kernel     other long sequences (register-staged K/V tiles)
 //   attn_kernel      everything else (nk <= 32, d > 160: the VAE mid attention)
@@ -851,6 +852,111 @@ __global__ void __launch_bounds__(NT, 4) attn_seq_kernel(AttnArgs a, int H, int 
   }
 }
 
+// attn_seqm: the same short-sequence attention on the matrix cores.  A block owns one
+// (pixel) sequence -- K and V rows of all heads staged in LDS exactly as above -- and
+// each wave takes whole (sequence, head) pairs: S^T = K Q^T as ceil(D/32) 16x16x32
+// MFMAs (B = Q^T straight from global, 64-B row segments), the 16 keys of a query
+// held 4 per lane so the softmax is 4 registers + two cross-row swaps, and
+// O^T = V^T P^T as ceil(D/16) 16x16x16 MFMAs whose B operand is the bf16 P already
+// in place and whose A operand comes from ds_read_b64_tr_b16.  Per (pixel, head)
+// that is ~60 wave instructions where the dot-product kernel spends ~450, which
+// leaves the kernel bound by the q/k/v/o stream.
+// Host contract: nq == nk <= 16, heads <= 8 (two per wave), heads contiguous,
+// D in {40, 80}, rows 8-element aligned (16-B loads, 8-B stores).
+template <int D>
+__global__ void __launch_bounds__(256) attn_seqm_kernel(AttnArgs a, int H, int nbatch) {
+  constexpr int KC = (D + 31) / 32, ND = (D + 15) / 16;
+  const int C = H * D, P = C + 8;  // LDS row pitch (elements)
+  const int F = a.nk;
+  extern __shared__ __attribute__((aligned(16))) u16 sm[];
+  u16* Ks = sm;           // [16][P]
+  u16* Vs = sm + 16 * P;  // [16][P]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lq = lane & 15, lg = lane >> 4;
+  const int bz = blockIdx.x;
+  if (bz >= nbatch) return;
+  const long b1 = bz / a.z2, b2 = bz - b1 * a.z2;
+
+  // Q^T fragments (B operand) of this wave's heads wid and wid + 4, issued first
+  bf16x8 qf[2][KC];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int h = wid + 4 * i;
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      const int d = kc * 32 + lg * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (h < H && lq < F && d < D)
+        v = *(const uint4*)(a.q + b1 * a.q_sb1 + b2 * a.q_sb2 + (long)lq * a.q_si + (long)h * D + d);
+      qf[i][kc] = __builtin_bit_cast(bf16x8, v);
+    }
+  }
+
+  // stage the sequence's K and V rows (zero rows past F)
+  const int cpr = C / 8;
+  for (int i = tid; i < 16 * cpr; i += 256) {
+    const int j = i / cpr, c8 = (i - j * cpr) * 8;
+    uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+    if (j < F) {
+      kv = *(const uint4*)(a.k + b1 * a.k_sb1 + b2 * a.k_sb2 + (long)j * a.k_si + c8);
+      vv = *(const uint4*)(a.v + b1 * a.v_sb1 + b2 * a.v_sb2 + (long)j * a.v_si + c8);
+    }
+    *(uint4*)(Ks + j * P + c8) = kv;
+    *(uint4*)(Vs + j * P + c8) = vv;
+  }
+  __syncthreads();
+
+  const int qq = lq >> 2, pp = lq & 3;
+  u16* ob = a.o + b1 * a.o_sb1 + b2 * a.o_sb2 + (long)lq * a.o_si;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int h = wid + 4 * i;
+    if (h >= H) break;
+    // s[r] = score(key 4 lg + r, query lq)
+    f32x4 s = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      const int d = kc * 32 + lg * 8;
+      uint4 kv = *(const uint4*)(Ks + lq * P + h * D + (d < D ? d : 0));
+      if (d >= D) kv = make_uint4(0, 0, 0, 0);  // past the head (pad / next head)
+      s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kv), qf[i][kc], s, 0, 0, 0);
+    }
+    float mt = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s[r] = 4 * lg + r < F ? s[r] * a.scale_log2 : -INFINITY;
+      mt = fmaxf(mt, s[r]);
+    }
+    mt = xor16_32_max(mt);
+    float l = 0.f;
+    v4i16 pb;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      // probabilities rounded to bf16 as the PV operand of a bf16 SDPA would be
+      const __bf16 p = (__bf16)fast_exp2(s[r] - mt);
+      l += (float)p;
+      pb[r] = __builtin_bit_cast(short, p);
+    }
+    const float inv = 1.f / xor16_32_sum(l);
+    const u16* va = Vs + (4 * lg + qq) * P + h * D + 4 * pp;
+#pragma unroll
+    for (int nd = 0; nd < ND; ++nd) {
+      const v4i16 vt = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)(va + nd * 16));
+      const f32x4 o = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vt, pb, (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      const int d = nd * 16 + 4 * lg;
+      if (lq < F && d < D)
+        *(uint2*)(ob + h * D + d) = make_uint2(pack2(o[0] * inv, o[1] * inv), pack2(o[2] * inv, o[3] * inv));
+    }
+  }
+}
+
+template <int D>
+static int launch_seqm(const AttnArgs& a, int batch, int heads, hipStream_t s) {
+  const size_t shm = (size_t)2 * 16 * (heads * D + 8) * sizeof(u16);
+  attn_seqm_kernel<D><<<batch, 256, shm, s>>>(a, heads, batch);
+  return check_launch("attn_seqm_kernel");
+}
+
 template <int D, int TS, int NT>
 static int launch_seq(const AttnArgs& a, int batch, int heads, hipStream_t s) {
   const int nb = NT / (heads * 16 * TS);
@@ -872,6 +978,7 @@ using namespace ls;
 
 static bool g_attn_v1 = getenv("LS_ATTN_V1") != nullptr;  // A/B switch: force the 16-query kernel
 static bool g_attn_v3 = getenv("LS_ATTN_V3") != nullptr;  // A/B switch: attn3 for d = 40 too
+static bool g_seq_valu = getenv("LS_ATTN_SEQ_VALU") != nullptr;  // A/B switch: dot-product short-sequence kernel
 
 extern "C" int ls_attention(const ls_attn_desc* d, void* stream) {
   if (!d || !d->q || !d->k || !d->v || !d->o) return fail(LS_ERR_INVALID, "ls_attention: null pointer");
@@ -899,6 +1006,8 @@ extern "C" int ls_attention(const ls_attn_desc* d, void* stream) {
                          (((uintptr_t)d->q | (uintptr_t)d->k | (uintptr_t)d->v | (uintptr_t)d->o) & 15) == 0;
     if (!g_attn_v1 && d->nq == d->nk && d->nk <= 16 && heads_packed && aligned && D % 40 == 0 &&
         (TS == 1 || TS == 2 || TS == 4) && H * 16 * TS <= 512 && 512 % (H * 16 * TS) == 0) {
+      if (!g_seq_valu && (D == 40 || D == 80) && H <= 8)
+        return D == 40 ? launch_seqm<40>(a, d->batch, H, s) : launch_seqm<80>(a, d->batch, H, s);
       // 256-thread blocks (several per CU desynchronise the load and compute phases)
       // wherever one (sequence, head) set fits
       const bool small_blk = H * 16 * TS <= 256 && 256 % (H * 16 * TS) == 0;
