@@ -56,7 +56,7 @@ PEAK_BF16_TF = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PRESETS = {
     1: dict(resolution=256, guidance=1.0, steps=20, windows=16),
     2: dict(resolution=256, guidance=2.0, steps=50, windows=8),
-    4: dict(resolution=512, guidance=1.0, steps=20, windows=2),
+    4: dict(resolution=512, guidance=1.0, steps=20, windows=2, attn="fp8"),
 }
 
 
@@ -380,6 +380,7 @@ def worker(args):
         from latentsync_amd.unet import UNet3DConditionModel
         from latentsync_amd.vae import AutoencoderKL
         unet = UNet3DConditionModel(**STAGE2_MODEL).init_weights(41).to(device).eval()
+        unet.set_attention_precision(args.attn_precision)
         vae = AutoencoderKL().init_weights(51).to(device)
         sched = DDIMScheduler(**SCHED_CFG)
         eng = WindowEngine(unet, vae, sched, F, R, args.inference_steps, args.guidance,
@@ -441,7 +442,9 @@ def worker(args):
         "vs_baseline": None, "dtype": "bf16", "data": "synthetic (seeded faces/audio/noise, random-init weights)",
         "config": {"workload": f"configs[{args.config}]: {R}x{R} x16-frame windows, "
                                f"{args.inference_steps} DDIM steps, guidance {args.guidance}, "
-                               "LatentSync-1.5 UNet + SD-VAE, bf16; "
+                               "LatentSync-1.5 UNet + SD-VAE, bf16"
+                               + ("; spatial self-attention P.V in fp8 e4m3 (block-scaled MFMA)"
+                                  if args.attn_precision == "fp8" else "") + "; "
                                f"{nw} independent windows of a clip batched per UNet call",
                    "windows_per_rank": K * nw, "windows_per_batch": nw, "frames_per_window": F,
                    "global_batch": world * nw * F, "resolution": R,
@@ -542,6 +545,8 @@ def parse_args():
                     help="BASELINE.json configs[i]: 1 = 256^2/20 steps/g 1.0 (headline), 2 = 50 steps/g 2.0 (CFG), "
                          "4 = 512^2/20 steps")
     ap.add_argument("--guidance", type=float, default=None)
+    ap.add_argument("--attn-precision", choices=("bf16", "fp8"), default=None,
+                    help="spatial self attention: bf16, or fp8 P.V (default: fp8 for configs[4], else bf16)")
     ap.add_argument("--inference-steps", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-whisper", action="store_true")
@@ -561,6 +566,8 @@ def parse_args():
         args.guidance = pre["guidance"]
     if args.inference_steps is None:
         args.inference_steps = pre["steps"]
+    if args.attn_precision is None:
+        args.attn_precision = pre.get("attn", "bf16")
     if args.windows_per_batch is None:
         args.windows_per_batch = pre["windows"] if not args.plumbing else 2
     args.resolution = pre["resolution"] if not args.plumbing else 8

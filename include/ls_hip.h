@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LS_ABI_VERSION 7
+#define LS_ABI_VERSION 8
 
 typedef enum {
   LS_OK = 0,
@@ -198,6 +198,21 @@ typedef struct {
 } ls_attn_desc;
 
 int ls_attention(const ls_attn_desc* d, void* stream);
+
+/*
+ * The same attention with the P V product in fp8 (BASELINE.json configs[4], "fp8 MFMA
+ * attention"; replaces the same SDPA call, attention.py:271): QK^T and the softmax as
+ * ls_attention (bf16 MFMA, fp32), P and V in OCP e4m3 on the block-scaled MFMA
+ * v_mfma_scale_f32_16x16x128_f8f6f4.  V is quantised by a pre-pass into `workspace`
+ * with one e8m0 scale per (head dim, 32 keys) -- MX block scaling, block max mapped
+ * into [128, 256); P (<= 2^8 by the kernel's rescale threshold) uses scale 1 and the
+ * row sums come from the same e4m3 P.  Two launches (quantise, attend), capturable.
+ * head_dim 40 or 80 (the UNet's 64^2 / 32^2 levels); q/k/v rows 16-B aligned, o rows 8-B aligned.
+ * Workspace: ls_attention_fp8_workspace_bytes(d) (0 = unsupported head_dim), 16-B aligned;
+ * its layout is documented in ls_attn.hip (the tests read it back).
+ */
+size_t ls_attention_fp8_workspace_bytes(const ls_attn_desc* d);
+int ls_attention_fp8(const ls_attn_desc* d, void* workspace, size_t workspace_bytes, void* stream);
 
 /*
  * Small-M linear in fp32: y[m, n] = sum_k act(x[m, k]) * W[n, k] + bias[n]

@@ -10,7 +10,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LS_HIP_LIB", os.path.join(HERE, "libls_hip.so"))
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 c_u16p = C.c_void_p
 c_vp = C.c_void_p
@@ -66,6 +66,8 @@ _SIGS = {
                                c_vp, c_vp]),
     "ls_row_stats": (C.c_int, [c_vp, C.c_int64, C.c_int64, C.c_int32, C.c_float, c_vp, c_vp]),
     "ls_attention": (C.c_int, [C.POINTER(AttnDesc), c_vp]),
+    "ls_attention_fp8_workspace_bytes": (C.c_size_t, [C.POINTER(AttnDesc)]),
+    "ls_attention_fp8": (C.c_int, [C.POINTER(AttnDesc), c_vp, C.c_size_t, c_vp]),
     "ls_small_linear": (C.c_int, [c_vp, C.c_int32, C.c_int32, c_vp, c_vp, C.c_int32, C.c_int32, c_vp, c_vp]),
     "ls_timestep_embed": (C.c_int, [c_vp, c_vp, C.c_int32, C.c_int32, C.c_int32, C.c_float, c_vp, c_vp]),
     "ls_ddim_cfg_step": (C.c_int, [c_vp, C.c_int32, C.c_int32, C.c_int64, C.c_float, c_vp, c_vp, c_vp, c_vp,

@@ -24,6 +24,7 @@
 #include "ls_common.h"
 
 typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef int v8i32 __attribute__((ext_vector_type(8)));
 
 namespace ls {
 
@@ -972,6 +973,388 @@ static int launch_seq(const AttnArgs& a, int batch, int heads, hipStream_t s) {
   return check_launch("attn_seq_kernel");
 }
 
+// ------------------------------------------------- fp8 P V (configs[4])
+// attn8: attn5's scheme with the P V product on the block-scaled fp8 MFMA
+// (v_mfma_scale_f32_16x16x128_f8f6f4, e4m3 x e4m3, fp32 accumulate: twice the bf16
+// rate per clock and a quarter of the PV instructions).  QK^T stays on bf16 MFMA:
+// at d = 40 the K = 128 fp8 shape would pad the head dim 3.2x, and the softmax is
+// the precision-sensitive half.
+//
+// Operands of O^T += V^T P^T over a 128-key tile, per lane (lq = lane & 15,
+// lg = lane >> 4): element j of the 32-byte fragment is key 16 (j >> 2) + 4 lg + (j & 3)
+// -- exactly the 32 scores the lane already holds in S^T (keys 16 f + 4 lg + r), so P
+// is packed in place (v_cvt_pk_fp8_f32, 16 per 16 queries) with no data movement.
+//   P  (B operand): e4m3 with scale 1.  The reference "max" m is an integer 7 below the
+//      ceil of the largest score seen when it last moved, so a fresh maximum has p in
+//      (2^6, 2^7] and e4m3's normal range (down to 2^-6) reaches 2^-13 below it (with
+//      m = max, everything under 2^-6 of the max -- a quarter of a flat softmax row --
+//      would sit in e4m3's 2^-9-step subnormals: 1-2 % output error on its own).  m moves
+//      when a tile max exceeds it by more than 8, so p <= 2^8 < 448 (e4m3 max).  Being an
+//      integer, m only scales every p by a power of two, which e4m3 rounds identically:
+//      the result does not depend on the order keys arrive in.
+//   V^T (A operand): quantised by vt8_quant_kernel into the caller's workspace, one
+//      e8m0 scale per (head dim, 128-key tile) with the row max mapped into [128, 256).
+//      Every lane group of a row passes the same scale: a finer per-32-key scale would
+//      tie the result to which k the hardware groups under one scale, and a lane-group
+//      assignment that differs from it was measured wrong (67 % error) on the box.  Row D
+//      is the constant 1.0 column, so O^T row D accumulates sum_k p_k of the same e4m3 p
+//      the numerator uses.
+// Workspace layout per (batch, head) pair: ceil(nk / 128) tiles of
+//   [ND * 16 rows][128 B]  e4m3, row d at d * 128, 16-B chunk c stored at chunk
+//                          c ^ ((d >> 1) & 7) (conflict-free ds_read_b128 of 16 rows)
+//   [ceil(ND / 4)][64 lanes][4] e8m0 scales: byte nd & 3 of lane (lg, lq)'s dword in
+//                          block nd >> 2 is the scale of row 16 nd + lq (equal for all lg)
+// so one tile is a contiguous run the attention kernel DMAs straight into LDS.
+template <int D>
+struct Fp8Tile {
+  static constexpr int KC = (D + 31) / 32;       // 32-wide QK^T k-steps (bf16)
+  static constexpr int ND = (D + 16) / 16;       // 16-row O^T fragments incl. the sum row
+  static constexpr int CPR = D / 8;              // 16-B chunks per K row
+  static constexpr int VBYTES = ND * 16 * 128;
+  static constexpr int NSC = (ND + 3) / 4;
+  static constexpr int TB = VBYTES + NSC * 256;  // workspace bytes per tile
+};
+
+__device__ __forceinline__ int fp8_key_of(int lg, int j) { return 16 * (j >> 2) + 4 * lg + (j & 3); }
+
+// e4m3 x e4m3 block-scaled MFMA, A scale = byte `sel` of sa (sel folds to an immediate
+// after unrolling), B scale 2^0
+__device__ __forceinline__ f32x4 mfma_fp8_mx(const v8i32& a, const v8i32& b, f32x4 c, int sel, int sa) {
+  switch (sel) {
+    case 0: return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, sa, 0, 127);
+    case 1: return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 1, sa, 0, 127);
+    case 2: return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 2, sa, 0, 127);
+    default: return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 3, sa, 0, 127);
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(256) vt8_quant_kernel(AttnArgs a, uint8_t* ws, long pair_bytes, int heads) {
+  using T = Fp8Tile<D>;
+  constexpr int R = T::ND * 16;
+  constexpr int PITCH = D + 2;  // odd word pitch: column reads are conflict-free
+  __shared__ u16 vs[128 * PITCH];
+  const int t = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const long b1 = b / a.z2, b2 = b - b1 * a.z2;
+  const u16* vb = a.v + b1 * a.v_sb1 + b2 * a.v_sb2 + (long)h * a.v_sh;
+  uint8_t* tile = ws + ((long)b * heads + h) * pair_bytes + (long)t * T::TB;
+  const int t0 = t * 128;
+  for (int i = threadIdx.x; i < 128 * T::CPR; i += 256) {
+    const int r = i / T::CPR, c = i - r * T::CPR;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (t0 + r < a.nk) v = *(const uint4*)(vb + (long)(t0 + r) * a.v_si + c * 8);
+    uint32_t* dst = (uint32_t*)(vs + r * PITCH + c * 8);
+    dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
+  }
+  __syncthreads();
+  // item (d, lg) = thread 4 d + lg: the 4 lane-group blocks of a row sit in adjacent
+  // lanes, so the row max is two xor shuffles
+  for (int base = 0; base < 4 * R; base += 256) {
+    const int it = base + threadIdx.x;
+    const int d = it >> 2, lg = it & 3;
+    float v[32];
+    float amax = 0.f;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      v[j] = d < D ? bf2f(vs[fp8_key_of(lg, j) * PITCH + d]) : 0.f;
+      amax = fmaxf(amax, fabsf(v[j]));
+    }
+    amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+    amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+    if (d >= R) continue;
+    uint32_t w[8];
+    int e8 = 127;
+    if (d < D) {
+      // row max into [128, 256): floor(log2 amax) - 7 (denormal / zero rows: 2^-127)
+      const int ex = (int)((__float_as_uint(amax) >> 23) & 0xff) - 127;
+      const int e = amax > 0.f ? ex - 7 : -127;
+      e8 = max(0, min(254, e + 127));
+      const float inv_s = __uint_as_float((uint32_t)(254 - e8) << 23);  // 2^(127 - e8), e8 <= 247
+#pragma unroll
+      for (int f = 0; f < 8; ++f) {
+        int p = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * f] * inv_s, v[4 * f + 1] * inv_s, 0, false);
+        w[f] = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[4 * f + 2] * inv_s, v[4 * f + 3] * inv_s, p, true);
+      }
+    } else {
+      const uint32_t c = d == D ? 0x38383838u : 0u;  // e4m3 1.0: the row-sum column
+#pragma unroll
+      for (int f = 0; f < 8; ++f) w[f] = c;
+    }
+    uint8_t* row = tile + d * 128;
+    const int sw = (d >> 1) & 7;
+    *(uint4*)(row + (((2 * lg) ^ sw) << 4)) = make_uint4(w[0], w[1], w[2], w[3]);
+    *(uint4*)(row + (((2 * lg + 1) ^ sw) << 4)) = make_uint4(w[4], w[5], w[6], w[7]);
+    const int nd = d >> 4, lq = d & 15;
+    tile[T::VBYTES + (nd >> 2) * 256 + (lg * 16 + lq) * 4 + (nd & 3)] = (uint8_t)e8;
+  }
+}
+
+template <int D, int QG, int NST, bool SB = true, int OCC = 2>
+__global__ void __launch_bounds__(256, OCC) attn8_kernel(AttnArgs a, const uint8_t* ws, long pair_bytes, int nqb,
+                                                       int heads) {
+  using T = Fp8Tile<D>;
+  constexpr int KC = T::KC, ND = T::ND, CPR = T::CPR;
+  constexpr int KT = 128;
+  constexpr int KPL = KC * 4;                       // K planes per 64-key half
+  constexpr int PLANE = 64 * 8;                     // u16 per plane (64 keys x 16 B)
+  constexpr int KBYTES = 2 * KPL * PLANE * 2;
+  constexpr int STAGE = KBYTES + T::TB;             // bytes
+  constexpr int NJ = 2 * CPR + 2 * ND + T::NSC;     // DMA instructions per tile
+  constexpr int NDMA = (NJ + 3) / 4;                // per wave (dummies pad the rest)
+  constexpr float TAU = 8.f;                        // p <= 2^8 < 448 (e4m3 max)
+  constexpr int DSUM = D;
+  static_assert(NST == 2 || NST == 3, "ring depth");
+  extern __shared__ __attribute__((aligned(16))) uint8_t smb[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lb = attn_xcd_remap(blockIdx.x, gridDim.x);
+  const int qblk = lb % nqb, pair = lb / nqb;
+  const int h = pair % heads;
+  const int b = pair / heads;
+  const long b1 = b / a.z2, b2 = b - b1 * a.z2;
+  const u16* qb = a.q + b1 * a.q_sb1 + b2 * a.q_sb2 + (long)h * a.q_sh;
+  const u16* kb = a.k + b1 * a.k_sb1 + b2 * a.k_sb2 + (long)h * a.k_sh;
+  u16* ob = a.o + b1 * a.o_sb1 + b2 * a.o_sb2 + (long)h * a.o_sh;
+  const uint8_t* wsp = ws + (long)pair * pair_bytes;
+  const int q0 = (qblk * 4 + wid) * 16 * QG;
+  const int lq = lane & 15, lg = lane >> 4;
+
+  // K planes past the head dim: zero in every stage and both halves
+  for (int i = tid; i < NST * 2 * (KPL - CPR) * 64; i += 256) {
+    const int r = i % 64, c = CPR + (i / 64) % (KPL - CPR), hf = (i / (64 * (KPL - CPR))) % 2,
+              st = i / (64 * (KPL - CPR) * 2);
+    *(uint4*)(smb + st * STAGE + ((hf * KPL + c) * PLANE + r * 8) * 2) = make_uint4(0, 0, 0, 0);
+  }
+
+  const float c2 = a.scale_log2;
+  bf16x8 qf[QG][KC];
+#pragma unroll
+  for (int g = 0; g < QG; ++g)
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      const int d = kc * 32 + lg * 8;
+      const int q = q0 + g * 16 + lq;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (q < a.nq && d < D) v = *(const uint4*)(qb + (long)q * a.q_si + d);
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] *= c2;
+      qf[g][kc] = __builtin_bit_cast(bf16x8, pack8(f));
+    }
+
+  const uint32_t kst = (uint32_t)a.k_si * 2;
+  const i32x4 krs = buffer_rsrc(kb, (uint32_t)(a.nk - 1) * kst + CPR * 16);
+  const i32x4 wrs = buffer_rsrc(wsp, (uint32_t)pair_bytes);
+  uint8_t* dummy = smb + NST * STAGE;
+  auto issue = [&](int t) {
+    uint8_t* st = smb + (t % NST) * STAGE;
+#pragma unroll
+    for (int u = 0; u < NDMA; ++u) {
+      const int j = wid + 4 * u;  // wave-uniform job
+      if (j < 2 * CPR) {
+        const int hf = j / CPR, c = j - hf * CPR;
+        ls_raw_buffer_load_lds(krs, (__attribute__((address_space(3))) void*)(st + (hf * KPL + c) * PLANE * 2), 16,
+                               lane * (int)kst + c * 16, (t * KT + 64 * hf) * (int)kst, 0, 0);
+      } else if (j < 2 * CPR + 2 * ND) {
+        const int i = j - 2 * CPR;
+        ls_raw_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(st + KBYTES + i * 1024), 16, lane * 16,
+                               t * T::TB + i * 1024, 0, 0);
+      } else if (j < NJ) {
+        const int i = j - 2 * CPR - 2 * ND;
+        ls_raw_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(st + KBYTES + T::VBYTES + i * 256), 4,
+                               lane * 4, t * T::TB + T::VBYTES + i * 256, 0, 0);
+      } else {
+        ls_raw_buffer_load_lds(krs, (__attribute__((address_space(3))) void*)dummy, 16, lane * (int)kst,
+                               t * KT * (int)kst, 0, 0);
+      }
+    }
+  };
+
+  f32x4 oacc[QG][ND];
+#pragma unroll
+  for (int g = 0; g < QG; ++g)
+#pragma unroll
+    for (int i = 0; i < ND; ++i) oacc[g][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // running reference max m (an integer), subtracted through the MFMA's C operand
+  float m[QG];
+  f32x4 negm[QG];
+#pragma unroll
+  for (int g = 0; g < QG; ++g) {
+    m[g] = 0.f;
+    negm[g] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+
+  const int ntile = (a.nk + KT - 1) / KT;
+  issue(0);
+  if (NST == 3 && ntile > 1) issue(1);
+  auto tile = [&](int t, auto partial_tag) {
+    constexpr bool PARTIAL = decltype(partial_tag)::value;
+    const int t0 = t * KT;
+    if (NST == 3 && t + 1 < ntile) attn_wait_vm<NDMA>();  // tile t landed; t+1 may fly
+    else attn_wait_vm<0>();
+    __syncthreads();                                      // everyone's; slot (t-1) % NST free
+    if (t + NST - 1 < ntile) issue(t + NST - 1);
+    const uint8_t* st = smb + (t % NST) * STAGE;
+    const u16* Ks = (const u16*)st;
+    const uint8_t* Vt = st + KBYTES;
+    const uint32_t* Sc = (const uint32_t*)(st + KBYTES + T::VBYTES);
+    auto pv = [&](const v8i32* pkv) {
+#pragma unroll
+    for (int nd = 0; nd < ND; ++nd) {
+      const int d = 16 * nd + lq;
+      const uint8_t* row = Vt + d * 128;
+      const int sw = (d >> 1) & 7;
+      const uint4 lo = *(const uint4*)(row + (((2 * lg) ^ sw) << 4));
+      const uint4 hi = *(const uint4*)(row + (((2 * lg + 1) ^ sw) << 4));
+      const v8i32 va = {(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+      const int sc = (int)Sc[(nd >> 2) * 64 + lane];
+#pragma unroll
+      for (int g = 0; g < QG; ++g)
+        oacc[g][nd] = mfma_fp8_mx(va, pkv[g], oacc[g][nd], nd & 3, sc);
+    }
+    };
+    // two 64-key halves: scores of one half live in registers at a time (QG * 16
+    // VGPRs); each half's P goes to e4m3 at once (8 bytes per f32x4 of scores)
+    v8i32 pk[QG];
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      bool first = t == 0 && hf == 0;
+      f32x4 s[QG][4];
+      auto qk = [&]() {
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+          const bf16x8 kf = __builtin_bit_cast(
+              bf16x8, *(const uint4*)(Ks + (hf * KPL + kc * 4 + lg) * PLANE + (16 * f + lq) * 8));
+#pragma unroll
+          for (int g = 0; g < QG; ++g)
+            s[g][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[g][kc], kc == 0 ? negm[g] : s[g][f], 0,
+                                                              0, 0);
+        }
+      }
+      };
+      qk();
+      bool again;
+      {
+        float mt[QG];
+        bool need_any = first;
+#pragma unroll
+        for (int g = 0; g < QG; ++g) {
+          if (PARTIAL) {
+#pragma unroll
+            for (int f = 0; f < 4; ++f)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (t0 + 64 * hf + 16 * f + 4 * lg + r >= a.nk) s[g][f][r] = -INFINITY;
+          }
+          float x = __builtin_elementwise_maximum(__builtin_elementwise_maximum(s[g][0][0], s[g][0][1]),
+                                                  __builtin_elementwise_maximum(s[g][0][2], s[g][0][3]));
+#pragma unroll
+          for (int f = 1; f < 4; ++f)
+            x = __builtin_elementwise_maximum(
+                x, __builtin_elementwise_maximum(__builtin_elementwise_maximum(s[g][f][0], s[g][f][1]),
+                                                 __builtin_elementwise_maximum(s[g][f][2], s[g][f][3])));
+          mt[g] = xor16_32_max(x);
+          need_any |= mt[g] > TAU;
+        }
+        again = __builtin_amdgcn_ballot_w64(need_any) != 0;
+        if (again) {
+          if (hf == 1) {
+            // the first half's P was packed against the old m: accumulate it now (second
+            // half zero) so the rescale below applies to it
+#pragma unroll
+            for (int g = 0; g < QG; ++g)
+#pragma unroll
+              for (int f = 4; f < 8; ++f) pk[g][f] = 0;
+            pv(pk);
+#pragma unroll
+            for (int g = 0; g < QG; ++g)
+#pragma unroll
+              for (int f = 0; f < 4; ++f) pk[g][f] = 0;
+          }
+#pragma unroll
+          for (int g = 0; g < QG; ++g) {
+            const bool need = first || mt[g] > TAU;
+            // new m: an integer 7 below the ceil of the tile max (its p in (2^6, 2^7])
+            const float dlt = need ? ceilf(mt[g]) - 7.f : 0.f;
+            const float alpha = first ? 0.f : fast_exp2(-dlt);
+            m[g] += dlt;
+            negm[g] = (f32x4){-m[g], -m[g], -m[g], -m[g]};
+#pragma unroll
+            for (int f = 0; f < 4; ++f) s[g][f] -= dlt;
+#pragma unroll
+            for (int i = 0; i < ND; ++i) oacc[g][i] *= alpha;
+          }
+          first = false;
+        }
+      }
+      // P^T in e4m3, element j = 4 f + r at byte j (key 16 f + 4 lg + r, f = 4 hf + f')
+#pragma unroll
+      for (int g = 0; g < QG; ++g)
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const int lo = __builtin_amdgcn_cvt_pk_fp8_f32(fast_exp2(s[g][f][0]), fast_exp2(s[g][f][1]), 0, false);
+          pk[g][4 * hf + f] = __builtin_amdgcn_cvt_pk_fp8_f32(fast_exp2(s[g][f][2]), fast_exp2(s[g][f][3]), lo, true);
+        }
+      if (SB) __builtin_amdgcn_sched_barrier(0);  // keep one half's scores live at a time
+    }
+    pv(pk);
+  };
+  const int nfull = a.nk / KT;
+  for (int t = 0; t < nfull; ++t) tile(t, std::false_type{});
+  if (nfull < ntile) tile(nfull, std::true_type{});
+#pragma unroll
+  for (int g = 0; g < QG; ++g) {
+    constexpr int NDL = DSUM / 16, LGL = (DSUM % 16) / 4, RL = DSUM % 4;
+    const float lt = __shfl(oacc[g][NDL][RL], LGL * 16 + lq, 64);
+    const float inv = 1.f / lt;
+    const int q = q0 + g * 16 + lq;
+    if (q < a.nq) {
+      u16* orow = ob + (long)q * a.o_si;
+#pragma unroll
+      for (int nd = 0; nd < ND; ++nd) {
+        const int d = nd * 16 + 4 * lg;
+        if (d + 3 < D) {
+          uint2 w;
+          w.x = (uint32_t)f2bf(oacc[g][nd][0] * inv) | ((uint32_t)f2bf(oacc[g][nd][1] * inv) << 16);
+          w.y = (uint32_t)f2bf(oacc[g][nd][2] * inv) | ((uint32_t)f2bf(oacc[g][nd][3] * inv) << 16);
+          *(uint2*)(orow + d) = w;
+        }
+      }
+    }
+  }
+}
+
+template <int D>
+static long fp8_pair_bytes(int nk) {
+  return (long)cdiv(nk, 128) * Fp8Tile<D>::TB;
+}
+
+template <int D, int QG, int NST, bool SB = true, int OCC = 2>
+static int launch_attn8(const AttnArgs& a, int batch, int heads, uint8_t* ws, hipStream_t s) {
+  using T = Fp8Tile<D>;
+  const long pb = fp8_pair_bytes<D>(a.nk);
+  if (pb >= (1L << 31)) return fail(LS_ERR_INVALID, "ls_attention_fp8: key set too long");
+  vt8_quant_kernel<D><<<dim3(cdiv(a.nk, 128), heads, batch), 256, 0, s>>>(a, ws, pb, heads);
+  int rc = check_launch("vt8_quant_kernel");
+  if (rc) return rc;
+  const int nqb = cdiv(a.nq, 4 * 16 * QG);
+  const long nblk = (long)nqb * heads * batch;
+  if (nblk > 0x7fffffff) return fail(LS_ERR_INVALID, "ls_attention_fp8: grid too large");
+  constexpr int STAGE = 2 * T::KC * 4 * 64 * 8 * 2 + T::TB;
+  const size_t shm = (size_t)NST * STAGE + 1024;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)attn8_kernel<D, QG, NST, SB, OCC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)shm);
+    attr_set = true;
+  }
+  attn8_kernel<D, QG, NST, SB, OCC><<<(int)nblk, 256, shm, s>>>(a, ws, pb, nqb, heads);
+  return check_launch("attn8_kernel");
+}
+
 }  // namespace ls
 
 using namespace ls;
@@ -980,11 +1363,7 @@ static bool g_attn_v1 = getenv("LS_ATTN_V1") != nullptr;  // A/B switch: force t
 static bool g_attn_v3 = getenv("LS_ATTN_V3") != nullptr;  // A/B switch: attn3 for d = 40 too
 static bool g_seq_valu = getenv("LS_ATTN_SEQ_VALU") != nullptr;  // A/B switch: dot-product short-sequence kernel
 
-extern "C" int ls_attention(const ls_attn_desc* d, void* stream) {
-  if (!d || !d->q || !d->k || !d->v || !d->o) return fail(LS_ERR_INVALID, "ls_attention: null pointer");
-  if (d->head_dim % 2 || d->head_dim <= 0 || d->head_dim > 512 || d->nq <= 0 || d->nk <= 0 || d->batch <= 0 ||
-      d->z2 <= 0 || d->heads <= 0)
-    return fail(LS_ERR_INVALID, "ls_attention: bad shape (head_dim even, <= 512)");
+static AttnArgs attn_args(const ls_attn_desc* d) {
   AttnArgs a;
   a.q = d->q; a.k = d->k; a.v = d->v; a.o = d->o;
   a.q_sb1 = d->q_sb1; a.q_sb2 = d->q_sb2; a.q_si = d->q_si; a.q_sh = d->q_sh;
@@ -993,6 +1372,58 @@ extern "C" int ls_attention(const ls_attn_desc* d, void* stream) {
   a.o_sb1 = d->o_sb1; a.o_sb2 = d->o_sb2; a.o_si = d->o_si; a.o_sh = d->o_sh;
   a.z2 = d->z2; a.nq = d->nq; a.nk = d->nk; a.D = d->head_dim;
   a.scale_log2 = d->scale * 1.4426950408889634f;
+  return a;
+}
+
+static int attn_check(const ls_attn_desc* d, const char* who) {
+  if (!d || !d->q || !d->k || !d->v || !d->o) return fail(LS_ERR_INVALID, std::string(who) + ": null pointer");
+  if (d->head_dim % 2 || d->head_dim <= 0 || d->head_dim > 512 || d->nq <= 0 || d->nk <= 0 || d->batch <= 0 ||
+      d->z2 <= 0 || d->heads <= 0)
+    return fail(LS_ERR_INVALID, std::string(who) + ": bad shape (head_dim even, <= 512)");
+  return LS_OK;
+}
+
+extern "C" size_t ls_attention_fp8_workspace_bytes(const ls_attn_desc* d) {
+  if (!d || d->nk <= 0 || d->batch <= 0 || d->heads <= 0) return 0;
+  const long pairs = (long)d->batch * d->heads;
+  switch (d->head_dim) {
+    case 40: return (size_t)(pairs * fp8_pair_bytes<40>(d->nk));
+    case 80: return (size_t)(pairs * fp8_pair_bytes<80>(d->nk));
+    default: return 0;
+  }
+}
+
+extern "C" int ls_attention_fp8(const ls_attn_desc* d, void* workspace, size_t workspace_bytes, void* stream) {
+  if (int rc = attn_check(d, "ls_attention_fp8")) return rc;
+  const int D = d->head_dim;
+  if (D != 40 && D != 80) return fail(LS_ERR_INVALID, "ls_attention_fp8: head_dim must be 40 or 80");
+  const bool aligned = d->q_si % 8 == 0 && d->k_si % 8 == 0 && d->v_si % 8 == 0 && d->q_sh % 8 == 0 &&
+                       d->k_sh % 8 == 0 && d->v_sh % 8 == 0 && d->q_sb1 % 8 == 0 && d->q_sb2 % 8 == 0 &&
+                       d->k_sb1 % 8 == 0 && d->k_sb2 % 8 == 0 && d->v_sb1 % 8 == 0 && d->v_sb2 % 8 == 0 &&
+                       (((uintptr_t)d->q | (uintptr_t)d->k | (uintptr_t)d->v) & 15) == 0 && d->o_si % 2 == 0 &&
+                       d->o_sh % 2 == 0 && d->o_sb1 % 2 == 0 && d->o_sb2 % 2 == 0 && ((uintptr_t)d->o & 7) == 0;
+  if (!aligned) return fail(LS_ERR_INVALID, "ls_attention_fp8: q/k/v rows must be 16-B aligned, o rows 8-B");
+  if (((long)d->nk + 128) * d->k_si * 2 >= (1L << 31)) return fail(LS_ERR_INVALID, "ls_attention_fp8: key set too long");
+  const size_t need = ls_attention_fp8_workspace_bytes(d);
+  if (!workspace || workspace_bytes < need || ((uintptr_t)workspace & 15))
+    return fail(LS_ERR_WORKSPACE, "ls_attention_fp8: workspace missing, unaligned or smaller than "
+                                  "ls_attention_fp8_workspace_bytes");
+  const AttnArgs a = attn_args(d);
+  hipStream_t s = (hipStream_t)stream;
+  uint8_t* ws = (uint8_t*)workspace;
+  static const int variant = getenv("LS_ATTN8_VARIANT") ? atoi(getenv("LS_ATTN8_VARIANT")) : 0;  // A/B switch
+  if (D == 40) {
+    if (variant == 1) return launch_attn8<40, 2, 2, false, 3>(a, d->batch, d->heads, ws, s);
+    if (variant == 2) return launch_attn8<40, 2, 2, true, 2>(a, d->batch, d->heads, ws, s);
+    if (variant == 3) return launch_attn8<40, 3, 3, true, 2>(a, d->batch, d->heads, ws, s);
+    return launch_attn8<40, 2, 2, true, 3>(a, d->batch, d->heads, ws, s);
+  }
+  return launch_attn8<80, 2, 2>(a, d->batch, d->heads, ws, s);
+}
+
+extern "C" int ls_attention(const ls_attn_desc* d, void* stream) {
+  if (int rc = attn_check(d, "ls_attention")) return rc;
+  const AttnArgs a = attn_args(d);
   hipStream_t s = (hipStream_t)stream;
   const bool small = d->nk <= 32;
   const int D = d->head_dim;

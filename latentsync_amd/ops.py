@@ -234,9 +234,12 @@ def layer_norm(x2d, gamma, beta, eps=1e-5, pe=None, pe_rows_per_frame=1, pe_fram
     return y
 
 
-def attention(q, k, v, o, *, batch, z2, heads, nq, nk, head_dim, qs, ks, vs, os_, scale=None):
+def attention(q, k, v, o, *, batch, z2, heads, nq, nk, head_dim, qs, ks, vs, os_, scale=None, fp8=False,
+              fp8_workspace=None):
     """qs/ks/vs/os_ = (sb1, sb2, si, sh) element strides; q/k/v/o base tensors
-    (may be offset views)."""
+    (may be offset views).  fp8=True: ls_attention_fp8 (P V on the block-scaled e4m3
+    MFMA, configs[4]); its V quantisation lands in `fp8_workspace` (uint8, allocated
+    here when None -- tests pass their own to read it back)."""
     lib = _lib.load()
     d = _lib.AttnDesc()
     d.q, d.k, d.v, d.o = _p(q), _p(k), _p(v), _p(o)
@@ -245,8 +248,24 @@ def attention(q, k, v, o, *, batch, z2, heads, nq, nk, head_dim, qs, ks, vs, os_
             setattr(d, f"{t}_{name}", int(val))
     d.batch, d.z2, d.heads, d.nq, d.nk, d.head_dim = batch, z2, heads, nq, nk, head_dim
     d.scale = scale if scale is not None else 1.0 / math.sqrt(head_dim)
+    if fp8:
+        n = lib.ls_attention_fp8_workspace_bytes(C.byref(d))
+        if n == 0:
+            raise ValueError(f"ls_attention_fp8: head_dim {head_dim} unsupported (40, 80)")
+        if fp8_workspace is None:
+            fp8_workspace = torch.empty(n, dtype=torch.uint8, device=q.device)
+        check(lib.ls_attention_fp8(C.byref(d), _p(fp8_workspace), fp8_workspace.numel(), _stream()),
+              "ls_attention_fp8")
+        return o
     check(lib.ls_attention(C.byref(d), _stream()), "ls_attention")
     return o
+
+
+def attention_fp8_workspace_bytes(*, batch, heads, nk, head_dim):
+    lib = _lib.load()
+    d = _lib.AttnDesc()
+    d.batch, d.z2, d.heads, d.nq, d.nk, d.head_dim = batch, 1, heads, 1, nk, head_dim
+    return lib.ls_attention_fp8_workspace_bytes(C.byref(d))
 
 
 def small_linear(x, w, bias, silu_in=False, out=None):

@@ -142,6 +142,7 @@ class _Resnet:
 class _Transformer:
     def __init__(self, dv, p, c, heads, groups, audio):
         self.c, self.heads, self.groups = c, heads, groups
+        self.fp8 = False  # spatial self attention's P V on the fp8 MFMA (configs[4])
         self.norm = (dv.f32(p + ".norm.weight"), dv.f32(p + ".norm.bias"))
         self.proj_in = dv.packed(p + ".proj_in.weight", p + ".proj_in.bias")
         self.proj_out = dv.packed(p + ".proj_out.weight", p + ".proj_out.bias")
@@ -175,7 +176,7 @@ class _Transformer:
         o = torch.empty((rows, C), dtype=torch.bfloat16, device=x.device)
         ops.attention(qkv, qkv[:, C:], qkv[:, 2 * C:], o, batch=n, z2=1, heads=self.heads, nq=HW, nk=HW, head_dim=d,
                       qs=(HW * 3 * C, 0, 3 * C, d), ks=(HW * 3 * C, 0, 3 * C, d), vs=(HW * 3 * C, 0, 3 * C, d),
-                      os_=(HW * C, 0, C, d))
+                      os_=(HW * C, 0, C, d), fp8=self.fp8 and HW > 128 and d in (40, 80))
         h = ops.linear(o, self.o1, res=h, stats_out=st)
         # audio cross attention
         if self.has_audio and audio_rows is not None:
@@ -330,6 +331,13 @@ class _DeviceUNet:
         self.temb_w = torch.cat(temb_w, 0).to(torch.bfloat16).to(device).contiguous()
         self.temb_b = torch.cat(temb_b, 0).float().to(device).contiguous()
 
+    def transformers(self):
+        for layers, _ in self.down + self.up:
+            for _, a, _ in layers:
+                if a is not None:
+                    yield a
+        yield self.mid[1]
+
     def temb(self, ts_i32, step_i32, B):
         t = ops.timestep_embed(ts_i32, step_i32, B, self.boc[0], self.flip, self.shift)
         e1 = ops.small_linear(t, self.t1, self.t1b)
@@ -434,6 +442,17 @@ class UNet3DConditionModel(torch.nn.Module):
     def from_config(cls, config):
         return cls(**dict(config))
 
+    def set_attention_precision(self, precision):
+        """'bf16' (default; the reference's SDPA at bf16) or 'fp8': the spatial
+        self attention (sequences > 128 tokens) computes P V on the block-scaled e4m3
+        MFMA (ls_attention_fp8) -- BASELINE.json configs[4].  Not a reference API."""
+        if precision not in ("bf16", "fp8"):
+            raise ValueError(f"attention precision {precision!r}: 'bf16' or 'fp8'")
+        self._attn_fp8 = precision == "fp8"
+        if self._dev is not None:
+            for a in self._dev.transformers():
+                a.fp8 = self._attn_fp8
+
     def set_attention_slice(self, slice_size):
         """Accepted for API compatibility (unet.py:243-306); the flash kernel never
         materialises the attention matrix, so slicing is a no-op."""
@@ -501,6 +520,8 @@ class UNet3DConditionModel(torch.nn.Module):
 
     def _pack(self):
         self._dev = _DeviceUNet(self._sd, self.config, self._device)
+        for a in self._dev.transformers():
+            a.fp8 = getattr(self, "_attn_fp8", False)
 
     def to(self, device=None, dtype=None, *a, **k):
         if isinstance(device, torch.dtype):

@@ -12,6 +12,11 @@ CASES = [  # name, batch(frames), tokens, keys, heads, d, kind
     ("cross L1 d80", 16 * W, 256, 50, 8, 80, "cross"), ("temporal L0 d40", W, 1024, 16, 8, 40, "temporal"),
     ("temporal L1 d80", W, 256, 16, 8, 80, "temporal"),
 ]
+if os.environ.get("CFG4"):  # configs[4]: 64^2 latent (WINDOWS windows of 16 frames)
+    CASES = [("c4 spatial L0 d40", 16 * W, 4096, 4096, 8, 40, "self"),
+             ("c4 spatial L1 d80", 16 * W, 1024, 1024, 8, 80, "self"),
+             ("c4 spatial L2 d160", 16 * W, 256, 256, 8, 160, "self")]
+FP8 = bool(os.environ.get("ATTN_FP8"))  # self attention through ls_attention_fp8
 
 
 def run():
@@ -34,7 +39,8 @@ def run():
             o = torch.empty_like(q)
             f = lambda: ops.attention(q, kv, kv[:, C:], o, batch=n, z2=1, heads=heads, nq=N, nk=Nk, head_dim=d,
                                       qs=(N * C, 0, C, d), ks=(Nk * 2 * C, 0, 2 * C, d),
-                                      vs=(Nk * 2 * C, 0, 2 * C, d), os_=(N * C, 0, C, d))
+                                      vs=(Nk * 2 * C, 0, 2 * C, d), os_=(N * C, 0, C, d),
+                                      fp8=FP8 and kind == "self" and d in (40, 80))
             flops = 4.0 * n * heads * N * Nk * d
         f()
         torch.cuda.synchronize()
@@ -54,7 +60,7 @@ def run():
             e0.record(); g.replay(); e1.record(); torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1) / 5)
         t = statistics.median(ts)
-        print(f"{os.environ.get('LS_ATTN_V1', 'v2'):3s} {name:18s} {t*1e3:9.1f} us {flops/t/1e9:8.1f} TF/s")
+        print(f"{'fp8' if FP8 and kind == 'self' else os.environ.get('LS_ATTN_V1', 'v2'):3s} {name:18s} {t*1e3:9.1f} us {flops/t/1e9:8.1f} TF/s")
         if kind != "temporal" and not os.environ.get("NO_SDPA"):  # torch SDPA (vendor flash attention) on the same problem, (B, H, N, d)
             qt = torch.randn(n, heads, N, d, device="cuda", dtype=torch.bfloat16)
             kt = torch.randn(n, heads, Nk, d, device="cuda", dtype=torch.bfloat16)

@@ -109,3 +109,41 @@ def test_full_size_window(vae, unet_full, guidance):
     assert int((_u8(out) - _u8(ref)).abs()[keep].max()) <= 1
     # the uint8 frames the engine hands to the gather / writer are the same pixels
     assert torch.equal(eng.out_u8.cpu().permute(0, 3, 1, 2).to(torch.int32), _u8(out))
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp8"])
+def test_configs4_window(vae, unet_full, precision):
+    """configs[4]: 512^2 (64^2 latent, spatial attention over 4096 tokens), stage2 UNet +
+    full VAE, 2 frames x 2 DDIM steps, with the spatial self attention in bf16 and in
+    fp8 (P V on the block-scaled e4m3 MFMA, the bench's configs[4] setting) against the
+    fp32 oracle (exact attention).  Same bounds as configs[1]: the fp8 attention error
+    (~4 % rel-L2 per attention output on random data, tests/test_gpu_fp8.py) is damped
+    by the out-projection + residual it feeds."""
+    from latentsync_amd.pipeline import WindowEngine, load_fixed_mask
+    from latentsync_amd.scheduler import DDIMScheduler
+    from oracle import ref_cpu as O
+    torch.set_num_threads(16)
+    Fr, R, steps = 2, 512, 2
+    h = R // 8
+    unet = unet_full
+    g = torch.Generator().manual_seed(11)
+    low = torch.rand((Fr, 3, R // 32, R // 32), generator=g)
+    faces = (torch.nn.functional.interpolate(low, size=(R, R), mode="bilinear") * 255).round().to(torch.uint8)
+    mask = load_fixed_mask(R)
+    audio = torch.randn((Fr, 50, 384), generator=g)
+    init = torch.randn((1, 4, 1, h, h), generator=g)
+    em, er = torch.randn((Fr, 4, h, h), generator=g), torch.randn((Fr, 4, h, h), generator=g)
+    unet.set_attention_precision(precision)
+    try:
+        eng = WindowEngine(unet, vae, DDIMScheduler(**SCHED), Fr, R, steps, 1.0)
+        eng.load(faces.cuda(), mask.cuda(), audio.cuda(), init.cuda(), em.cuda(), er.cuda())
+        out = eng.run().float().cpu()
+    finally:
+        unet.set_attention_precision("bf16")
+    with torch.no_grad():
+        ref = O.pipeline_window(unet.state_dict(), dict(unet.config), vae._sd, faces, mask, audio, init, em, er,
+                                num_steps=steps, guidance_scale=1.0)
+    e = rel_err(out, ref)
+    print(f"configs[4] window rel_err ({precision} attention)", e)
+    assert e < 3e-2
+    _pixel_check(out, ref, (mask < 1)[None, None])
