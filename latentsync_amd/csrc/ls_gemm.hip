@@ -1503,8 +1503,13 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
   constexpr int BM = 8 * 16 * FM;             // rows per workgroup (8 waves x FM fragments of 16)
   constexpr int KTILES = KT / 2;              // 64-wide LDS images per chunk
   constexpr int WIMG = BN * KTILES * 8;       // uint4 of the W images of a chunk
-  constexpr int STAGE = WIMG + 48;            // + bias / colsum / row-vector columns (3 x 64 fp32)
   constexpr bool LN = FLAGS & RB_LN, RES = FLAGS & RB_RES, RV = FLAGS & RB_RV, GG = FLAGS & RB_GEGLU;
+  // residual tile of a chunk (BM rows x BN columns bf16) DMA'd with its W images, so it is
+  // in flight two chunks ahead of its epilogue with no registers held (the register
+  // residual, one chunk ahead, left the short-K residual GEMMs latency-bound on HBM)
+  constexpr int RIMG = RES ? BM * BN / 8 : 0;  // uint4
+  constexpr int RPT = RIMG / 512;
+  constexpr int STAGE = WIMG + 48 + RIMG;     // + bias / colsum / row-vector columns (3 x 64 fp32) + residual
   constexpr bool AF = FLAGS & RB_AFF;  // GroupNorm affine (+SiLU) prologue on the register-resident A rows
   constexpr bool ST = (FLAGS & RB_STATS) && !GG;  // row statistics of the output (host: one N range per block)
   // GroupNorm column sums (a.cs_out): per chunk a wave's 16 FM rows are summed over its
@@ -1541,6 +1546,11 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
       const float* base = q == 0 ? a.bias : q == 1 ? nullptr : (RV ? a.rowvec + rv_base : nullptr);
       const void* ps = base ? (const void*)(base + c * BN + e) : (const void*)ls_zero_page;
       glds16(ps, dst + WIMG);
+    }
+#pragma unroll
+    for (int p = 0; p < RPT; ++p) {  // residual piece q: row q / (BN / 8), 16-B column chunk q % (BN / 8)
+      const int q = p * 512 + tid, row = q / (BN / 8), ch = q % (BN / 8);
+      glds16(a.res + (long)(rb * BM + row) * a.ldr + c * BN + ch * 8, dst + WIMG + 48 + p * 512 + wid * 64);
     }
   };
 
@@ -1604,18 +1614,6 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
   asm volatile("" ::: "memory");
 
   f32x4 acc0[FM][FN], acc1[FM][FN];
-  uint2 rsA[FM][FN], rsB[FM][FN];  // residual of the chunk being computed / of the one in its epilogue
-  constexpr int NRES = RES ? FM * FN : 0;
-
-  auto load_res = [&](int c, uint2 (&rs)[FM][FN]) {
-    if (!RES) return;
-    const int nb = c * BN + 4 * lg;
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        rs[i][j] = *(const uint2*)(a.res + (long)(mw + i * 16 + l16) * a.ldr + nb + 16 * j);
-  };
   // column parameters (bias + row vector) of chunk c from its LDS stage, read before
   // the next DMA is issued (an LDS read after it would wait for the DMA)
   auto load_prm = [&](int stage, float4 (&bb)[FN]) {
@@ -1632,8 +1630,9 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
   double S1[FM], S2[FM];  // running row sums of the output (ST), per lane: its 4-column slices
 #pragma unroll
   for (int i = 0; i < FM; ++i) { S1[i] = 0.0; S2[i] = 0.0; }
-  auto epilogue = [&](int c, const float4 (&bb)[FN], f32x4 (&acc)[FM][FN], const uint2 (&rs)[FM][FN]) {
+  auto epilogue = [&](int c, const float4 (&bb)[FN], f32x4 (&acc)[FM][FN], int stage) {
     const int nb = c * BN + 4 * lg;  // packed column of fragment j: nb + 16 j
+    const u16* rtile = (const u16*)(lds_dyn + stage * STAGE + WIMG + 48);  // [BM][BN] residual of chunk c
     float cs1[FM], cs2[FM];  // this chunk's partial sums (fp32 over 4*FN values), folded into S in fp64
     float gcs[FM][FN][4];    // stored values of this chunk (CS)
 #pragma unroll
@@ -1659,8 +1658,9 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
           float o[4];
           float r4[4] = {0.f, 0.f, 0.f, 0.f};
           if (RES) {
-            r4[0] = __uint_as_float(rs[i][j].x << 16); r4[1] = __uint_as_float(rs[i][j].x & 0xffff0000u);
-            r4[2] = __uint_as_float(rs[i][j].y << 16); r4[3] = __uint_as_float(rs[i][j].y & 0xffff0000u);
+            const uint2 rs = *(const uint2*)(rtile + (wid * 16 * FM + i * 16 + l16) * BN + 4 * lg + 16 * j);
+            r4[0] = __uint_as_float(rs.x << 16); r4[1] = __uint_as_float(rs.x & 0xffff0000u);
+            r4[2] = __uint_as_float(rs.y << 16); r4[3] = __uint_as_float(rs.y & 0xffff0000u);
           }
 #pragma unroll
           for (int r = 0; r < 4; ++r) o[r] = (acc[i][j][r] + r4[r]) * a.out_scale;
@@ -1743,40 +1743,37 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
   // 3-stage ring: chunk c computes from stage c%3 while chunk c-1's parameters stay in
   // (c-1)%3 for its epilogue and chunk c+1 lands in (c+1)%3.  Past the last chunk the DMA
   // re-loads the last chunk into the spare stage, so the steady-state body is branch-free.
-  // The residual of chunk c is loaded a whole chunk ahead of its epilogue, younger than
-  // the DMA, so the end-of-chunk wait (DMA landed) leaves it in flight.
-  auto body = [&](int c, f32x4 (&acc)[FM][FN], f32x4 (&prev)[FM][FN], uint2 (&rs_load)[FM][FN],
-                  uint2 (&rs_use)[FM][FN]) {
+  // The residual tile of chunk c travels with the chunk's W images (stage c % 3).
+  auto body = [&](int c, f32x4 (&acc)[FM][FN], f32x4 (&prev)[FM][FN]) {
     const int st = (c - c0) % 3;
+    const int sp = st == 0 ? 2 : st - 1;
     float4 bb[FN];
-    load_prm(st == 0 ? 2 : st - 1, bb);
+    load_prm(sp, bb);
     issue(min(c + 1, c1 - 1), st == 2 ? 0 : st + 1);
     if (CS && c - 2 >= c0) merge_cs(c - 2);  // written two epilogues ago, past a barrier
-    load_res(c, rs_load);
     mfma_chunk(st, acc);
-    epilogue(c - 1, bb, prev, rs_use);
-    wait_vm<NSTORE + NRES>();                                // the DMA (older than both) landed
+    epilogue(c - 1, bb, prev, sp);
+    wait_vm<NSTORE>();                                       // the DMA (older than the stores) landed
     sync();
   };
   // first chunk: no epilogue
   issue(min(c0 + 1, c1 - 1), 1);
-  load_res(c0, rsA);
   mfma_chunk(0, acc0);
-  wait_vm<NRES>();
+  wait_vm<0>();
   sync();
   int c = c0 + 1;
   for (; c + 1 < c1; c += 2) {
-    body(c, acc1, acc0, rsB, rsA);
-    body(c + 1, acc0, acc1, rsA, rsB);
+    body(c, acc1, acc0);
+    body(c + 1, acc0, acc1);
   }
   float4 bb[FN];
   if (c < c1) {
-    body(c, acc1, acc0, rsB, rsA);
+    body(c, acc1, acc0);
     load_prm((c - c0) % 3, bb);
-    epilogue(c, bb, acc1, rsB);
+    epilogue(c, bb, acc1, (c - c0) % 3);
   } else {
     load_prm((c1 - 1 - c0) % 3, bb);
-    epilogue(c1 - 1, bb, acc0, rsA);
+    epilogue(c1 - 1, bb, acc0, (c1 - 1 - c0) % 3);
   }
   if (CS) {  // the last two chunks' column sums
     __syncthreads();
@@ -1850,6 +1847,7 @@ static TileCfg pick_tile(long M, int N, int ktiles, bool allow_split, bool big_o
 // ---- row-block GEMM dispatch (gemm_rowblock_kernel)
 static bool g_rowblock = getenv("LS_GEMM_NO_ROWBLOCK") == nullptr;
 static bool g_rowblock640 = getenv("LS_GEMM_NO_ROWBLOCK640") == nullptr;
+static bool g_rb640_res = getenv("LS_GEMM_RB640_RES") != nullptr;  // A/B switch: K = 640 residual GEMMs too
 
 static bool rowblock_ok(const ls_conv_desc* d, const ConvArgs& a) {
   if (!g_rowblock || g_force_tile || g_force_regstage || d->ksize != 1 || a.C2) return false;
@@ -1859,12 +1857,12 @@ static bool rowblock_ok(const ls_conv_desc* d, const ConvArgs& a) {
     return false;
   // K = 640 only without a residual (the tiled kernel is faster there: 48 vs 53 us at 16x16)
   if (!((a.Cin == 320 && a.K == 320 && a.M % 256 == 0) ||
-        (g_rowblock640 && a.Cin == 640 && a.K == 640 && a.M % 128 == 0 && !a.res)))
+        (g_rowblock640 && a.Cin == 640 && a.K == 640 && a.M % 128 == 0 && (!a.res || g_rb640_res))))
     return false;
   if (a.N % 64 || a.split != 1 || a.y_f32) return false;
   if (a.act != LS_ACT_NONE && a.act != LS_ACT_GEGLU) return false;
-  if (a.ldy % 4 || (a.res && a.ldr % 4) || (a.rowvec && (a.rowvec_ld % 4 || a.rows_per_vec % 256))) return false;
-  if (((uintptr_t)a.y | (uintptr_t)a.res) & 7) return false;  // 8-B row pieces
+  if (a.ldy % 4 || (a.res && a.ldr % 8) || (a.rowvec && (a.rowvec_ld % 4 || a.rows_per_vec % 256))) return false;
+  if (((uintptr_t)a.y & 7) || ((uintptr_t)a.res & 15)) return false;  // 8-B output pieces, 16-B residual DMA
   return (((uintptr_t)a.x1 | (uintptr_t)a.bias | (uintptr_t)a.ln_cs | (uintptr_t)a.rowvec) & 15) == 0;
 }
 
@@ -1873,7 +1871,9 @@ static bool rowblock_ok(const ls_conv_desc* d, const ConvArgs& a) {
 template <int KT, int FM, int FLAGS>
 static void launch_rowblock2(const ConvArgs& a, int grid, hipStream_t s) {
   constexpr int FN = 2;
-  const size_t shm = (size_t)3 * (16 * FN * (KT / 2) * 8 + 48) * 16 + ((FLAGS & RB_GNCS) ? 4096 : 0);
+  constexpr int BM = 8 * 16 * FM;
+  const size_t shm = (size_t)3 * (16 * FN * (KT / 2) * 8 + 48 + ((FLAGS & RB_RES) ? BM * 16 * FN / 8 : 0)) * 16 +
+                     ((FLAGS & RB_GNCS) ? 4096 : 0);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gemm_rowblock_kernel<KT, FM, FN, FLAGS>,
