@@ -196,25 +196,38 @@ gn_colsum_finalize_kernel(const float* __restrict__ cs1, const float* __restrict
   }
 }
 
-// Materialised GroupNorm apply (+SiLU) over an optional channel concat.
-__global__ void gn_apply_kernel(const u16* __restrict__ x1, const u16* __restrict__ x2, int C1, int C2, long n_chunks,
-                                long pps, const float* __restrict__ scale, const float* __restrict__ shift, int silu_on,
-                                u16* __restrict__ y) {
+// Materialised GroupNorm apply (+SiLU) over an optional channel concat.  A thread keeps
+// one 8-channel chunk for its whole grid-stride walk over pixels (ppb pixels per block
+// pass, C / 8 threads each), so the loop has no 64-bit index division, and it re-reads
+// its scale / shift only when the walk crosses into the next sample.
+__global__ void __launch_bounds__(256) gn_apply_kernel(const u16* __restrict__ x1, const u16* __restrict__ x2, int C1,
+                                                       int C2, long n_pix, long pps, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, int silu_on,
+                                                       u16* __restrict__ y, int ppb, int ccb) {
+  // ppb pixels per block pass, ccb chunks of 8 channels per pixel (blockIdx.y selects which)
   const int C = C1 + C2, CC = C / 8;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n_chunks; i += (long)gridDim.x * blockDim.x) {
-    const long pix = i / CC;
-    const int c = (int)(i - pix * CC) * 8;
-    const long s = pix / pps;
-    const uint4 u = c < C1 ? *(const uint4*)(x1 + pix * C1 + c) : *(const uint4*)(x2 + pix * C2 + (c - C1));
-    const float4 s0 = *(const float4*)(scale + s * C + c), s1 = *(const float4*)(scale + s * C + c + 4);
-    const float4 h0 = *(const float4*)(shift + s * C + c), h1 = *(const float4*)(shift + s * C + c + 4);
-    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+  const int pl = threadIdx.x / ccb, cc = blockIdx.y * ccb + threadIdx.x - pl * ccb;
+  if (pl >= ppb || cc >= CC) return;
+  const int c = cc * 8;
+  const u16* src = c < C1 ? x1 + c : x2 + (c - C1);
+  const int lds = c < C1 ? C1 : C2;
+  long s_cur = -1, s_end = 0;
+  float sc[8], sh[8];
+  const long step = (long)gridDim.x * ppb;
+  for (long pix = (long)blockIdx.x * ppb + pl; pix < n_pix; pix += step) {
+    if (pix >= s_end || s_cur < 0) {  // entered another sample (rare: samples span many passes)
+      s_cur = pix / pps;
+      s_end = (s_cur + 1) * pps;
+      const float4 s0 = *(const float4*)(scale + s_cur * C + c), s1 = *(const float4*)(scale + s_cur * C + c + 4);
+      const float4 h0 = *(const float4*)(shift + s_cur * C + c), h1 = *(const float4*)(shift + s_cur * C + c + 4);
+      sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+      sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w; sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
+    }
     float f[8];
-    unpack8(u, f);
+    unpack8(*(const uint4*)(src + pix * lds), f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float t = f[j] * sc[j] + sh[j];
+      const float t = fmaf(f[j], sc[j], sh[j]);
       f[j] = silu_on ? silu(t) : t;
     }
     *(uint4*)(y + pix * C + c) = pack8(f);
@@ -335,9 +348,13 @@ extern "C" int ls_groupnorm_apply(const uint16_t* x1, const uint16_t* x2, int32_
                                   void* stream) {
   if (!x1 || !y || !scale || !shift || (C1 + C2) % 8 || C1 % 8 || n_pix <= 0 || pps <= 0 || (C2 && !x2))
     return fail(LS_ERR_INVALID, "ls_groupnorm_apply: bad arguments");
-  const long n = n_pix * ((C1 + C2) / 8);
-  gn_apply_kernel<<<(int)std::min<long>(cdiv(n, 256), 16384), 256, 0, (hipStream_t)stream>>>(
-      x1, x2, C1, C2, n, pps, scale, shift, silu_on, y);
+  const int CC = (C1 + C2) / 8;
+  const int ccb = std::min(CC, 256);
+  const int ppb = std::max(1, 256 / ccb);
+  const int threads = (ppb * ccb + 63) / 64 * 64;  // 1280 channels: 3 waves, 160 live lanes
+  const long blocks = std::min<long>(cdiv(n_pix, ppb), 16384);
+  gn_apply_kernel<<<dim3((unsigned)blocks, cdiv(CC, ccb)), threads, 0, (hipStream_t)stream>>>(
+      x1, x2, C1, C2, n_pix, pps, scale, shift, silu_on, y, ppb, ccb);
   return check_launch("gn_apply_kernel");
 }
 
