@@ -19,6 +19,7 @@ three captured hipGraphs replayed back to back --
 Random draws are injected (initial latent noise, VAE posterior noise), as the
 parity harness requires (SURVEY.md §7 "RNG").
 """
+import gc
 import math
 import os
 
@@ -140,9 +141,12 @@ class WindowEngine:
         self.lat.copy_(self.init_lat)
         ops.pack_unet_input(self.lat, self.cond, self.mask, self.FT, self.R, self.h, self.Bu, self.unet_in)
         self.step.zero_()
+        # audio cross-attention k|v of every Transformer3DModel: constant over the 20 steps
+        self.audio_kv = self.ud.audio_kv(self.audio)
 
     def _step(self):
-        eps = self.ud.forward(self.unet_in, self.Bu * self.nw, self.ts, self.step, self.audio, self.L)
+        eps = self.ud.forward(self.unet_in, self.Bu * self.nw, self.ts, self.step, self.audio, self.L,
+                              audio_kv=self.audio_kv)
         ops.ddim_cfg_step(eps, self.Bu, self.g, self.lat, self.coef, self.step, self.unet_in)
 
     def _decode(self):
@@ -158,11 +162,20 @@ class WindowEngine:
         torch.cuda.synchronize(self.device)
         pool = torch.cuda.graph_pool_handle()
         graphs = []
-        for fn in (self._encode, self._step, self._decode):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
-                fn()
-            graphs.append(g)
+        # no garbage collection while a stream is capturing: a collected engine's graphs
+        # would be destroyed mid-capture, which aborts the HIP runtime (torch.cuda.graph
+        # collects once on entry; the host code inside can create new cyclic garbage)
+        gc_was_on = gc.isenabled()
+        gc.disable()
+        try:
+            for fn in (self._encode, self._step, self._decode):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    fn()
+                graphs.append(g)
+        finally:
+            if gc_was_on:
+                gc.enable()
         torch.cuda.synchronize(self.device)
         self.graphs = graphs
 

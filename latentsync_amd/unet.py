@@ -160,7 +160,13 @@ class _Transformer:
                                 geglu=True)
         self.ff2 = dv.packed(b + ".ff.net.2.weight", b + ".ff.net.2.bias")
 
-    def __call__(self, x, audio_rows, n_audio_tok):
+    def audio_kv(self, audio_rows):
+        """The audio cross-attention k|v projection (attn2.to_k / to_v of the audio
+        embeddings).  It does not depend on the latents, so the window engine computes it
+        once per batch of windows instead of once per DDIM step."""
+        return ops.linear(audio_rows, self.kv2) if self.has_audio else None
+
+    def __call__(self, x, audio_rows, n_audio_tok, kv=None):
         n, H, W, C = x.shape
         HW = H * W
         rows = n * HW
@@ -181,7 +187,8 @@ class _Transformer:
         # audio cross attention
         if self.has_audio and audio_rows is not None:
             q = ops.linear(h, self.q2, ln_stats=st)
-            kv = ops.linear(audio_rows, self.kv2)
+            if kv is None:
+                kv = ops.linear(audio_rows, self.kv2)
             L = n_audio_tok
             ops.attention(q, kv, kv[:, C:], o, batch=n, z2=1, heads=self.heads, nq=HW, nk=L, head_dim=d,
                           qs=(HW * C, 0, C, d), ks=(L * 2 * C, 0, 2 * C, d), vs=(L * 2 * C, 0, 2 * C, d),
@@ -331,6 +338,13 @@ class _DeviceUNet:
         self.temb_w = torch.cat(temb_w, 0).to(torch.bfloat16).to(device).contiguous()
         self.temb_b = torch.cat(temb_b, 0).float().to(device).contiguous()
 
+    def audio_kv(self, audio_rows):
+        """k|v projections of the audio rows for every Transformer3DModel, in forward
+        order (down, mid, up) -- constant over the denoising loop."""
+        order = [a for layers, _ in self.down for _, a, _ in layers if a is not None] + [self.mid[1]] + \
+                [a for layers, _ in self.up for _, a, _ in layers if a is not None]
+        return {id(a): a.audio_kv(audio_rows) for a in order}
+
     def transformers(self):
         for layers, _ in self.down + self.up:
             for _, a, _ in layers:
@@ -344,8 +358,11 @@ class _DeviceUNet:
         emb = ops.small_linear(e1, self.t2, self.t2b, silu_in=True)
         return ops.small_linear(emb, self.temb_w, self.temb_b, silu_in=True)
 
-    def forward(self, x_in, B, ts_i32, step_i32, audio_rows, n_audio_tok, down_res=None, mid_res=None):
-        """x_in NHWC bf16 (B*F, H, W, cin_pad) -> eps NHWC bf16 (B*F, H, W, out_channels)."""
+    def forward(self, x_in, B, ts_i32, step_i32, audio_rows, n_audio_tok, down_res=None, mid_res=None,
+                audio_kv=None):
+        """x_in NHWC bf16 (B*F, H, W, cin_pad) -> eps NHWC bf16 (B*F, H, W, out_channels).
+        audio_kv: the dict of audio_kv(audio_rows), precomputed once per window batch."""
+        kvs = audio_kv or {}
         temb = self.temb(ts_i32, step_i32, B)
         h = ops.conv(x_in, self.conv_in, gn_out=True)
         skips = [h]
@@ -353,7 +370,7 @@ class _DeviceUNet:
             for r, a, m in layers:
                 h = r(h, B, temb)
                 if a is not None:
-                    h = a(h, audio_rows, n_audio_tok)
+                    h = a(h, audio_rows, n_audio_tok, kvs.get(id(a)))
                 if m is not None:
                     h = m(h, B)
                 skips.append(h)
@@ -364,7 +381,7 @@ class _DeviceUNet:
             skips = [s + r for s, r in zip(skips, down_res)]
         r0, a, m, r1 = self.mid
         h = r0(h, B, temb)
-        h = a(h, audio_rows, n_audio_tok)
+        h = a(h, audio_rows, n_audio_tok, kvs.get(id(a)))
         if m is not None:
             h = m(h, B)
         h = r1(h, B, temb)
@@ -374,7 +391,7 @@ class _DeviceUNet:
             for r, a, m in layers:
                 h = r(h, B, temb, x2=skips.pop())
                 if a is not None:
-                    h = a(h, audio_rows, n_audio_tok)
+                    h = a(h, audio_rows, n_audio_tok, kvs.get(id(a)))
                 if m is not None:
                     h = m(h, B)
             if us is not None:
