@@ -1,7 +1,7 @@
 """Benchmark: lip-synced frames/sec at 256x256, 16-frame window, 20 DDIM steps
 (BASELINE.json "metric", configs[1]; configs[3] when launched on N GPUs).
 
-One "step" = one batch of `--windows-per-batch` (default 16) independent
+One "step" = one batch of `--windows-per-batch` (default 32 at configs[1]) independent
 16-frame windows of a clip through the whole hot path on one GPU: pixel prep ->
 VAE encode x2 -> 20 x (UNet3D fwd + CFG + DDIM) -> VAE decode -> paste-back,
 inputs resident in HBM.  Every window is computed exactly as alone (per-window
@@ -52,11 +52,12 @@ PEAK_BF16_TF = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 # BASELINE.json configs this bench can run on one GPU (configs[0] is the CPU-only
 # plumbing case, configs[3] is configs[1] sharded over 8 ranks)
 # windows: independent 16-frame windows of a clip batched per UNet call (measured on MI355X:
-# 8 -> 110.2, 16 -> 113.3 frames/s at configs[1], profiles/r01f_bench.json)
+# 8 -> 110.2, 16 -> 113.3 frames/s at configs[1], profiles/r01f_bench.json; same box, round 2
+# (profiles/r02k_wpb_sweep.txt): 16 -> 121.4, 24 -> 122.9, 32 -> 123.2; configs[4] 2 -> 27.3, 4 -> 28.1)
 PRESETS = {
-    1: dict(resolution=256, guidance=1.0, steps=20, windows=16),
+    1: dict(resolution=256, guidance=1.0, steps=20, windows=32),
     2: dict(resolution=256, guidance=2.0, steps=50, windows=8),
-    4: dict(resolution=512, guidance=1.0, steps=20, windows=2, attn="fp8"),
+    4: dict(resolution=512, guidance=1.0, steps=20, windows=4, attn="fp8"),
 }
 
 
