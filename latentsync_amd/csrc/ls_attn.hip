@@ -13,6 +13,7 @@
 //
 // Kernels (dispatch in ls_attention):
 //   attn_seqm_kernel short sequences (the temporal attention over a window's frames), MFMA
+//                    (d = 80 / 160: a sequence's heads split over two blocks)
 //   attn_seq_kernel  the same with packed-bf16 dot products (d = 160, A/B baseline)
 //   attn5_kernel     d = 40 self attention: DMA-fed K/V planes, 64 queries per wave
 //   attn3_kernel     other long sequences (register-staged K/V tiles)
@@ -863,11 +864,15 @@ __global__ void __launch_bounds__(NT, 4) attn_seq_kernel(AttnArgs a, int H, int 
 // that is ~60 wave instructions where the dot-product kernel spends ~450, which
 // leaves the kernel bound by the q/k/v/o stream.
 // Host contract: nq == nk <= 16, heads <= 8 (two per wave), heads contiguous,
-// D in {40, 80}, rows 8-element aligned (16-B loads, 8-B stores).
-template <int D>
+// D in {40, 80, 160}, rows 8-element aligned (16-B loads, 8-B stores).  HS > 1 splits a
+// sequence's heads over HS blocks (blockIdx.y), each staging only its heads' channels:
+// d = 160 with all 8 heads would need 82 KB of LDS (one block per CU), 4 heads 41 KB.
+template <int D, int HS = 1>
 __global__ void __launch_bounds__(256) attn_seqm_kernel(AttnArgs a, int H, int nbatch) {
   constexpr int KC = (D + 31) / 32, ND = (D + 15) / 16;
-  const int C = H * D, P = C + 8;  // LDS row pitch (elements)
+  const int HB = H / HS;                        // heads of this block
+  const int C = HB * D, P = C + 8;              // staged channels, LDS row pitch (elements)
+  const int h0 = blockIdx.y * HB;
   const int F = a.nk;
   extern __shared__ __attribute__((aligned(16))) u16 sm[];
   u16* Ks = sm;           // [16][P]
@@ -882,13 +887,13 @@ __global__ void __launch_bounds__(256) attn_seqm_kernel(AttnArgs a, int H, int n
   bf16x8 qf[2][KC];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const int h = wid + 4 * i;
+    const int h = wid + 4 * i;  // head within the block
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
       const int d = kc * 32 + lg * 8;
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (h < H && lq < F && d < D)
-        v = *(const uint4*)(a.q + b1 * a.q_sb1 + b2 * a.q_sb2 + (long)lq * a.q_si + (long)h * D + d);
+      if (h < HB && lq < F && d < D)
+        v = *(const uint4*)(a.q + b1 * a.q_sb1 + b2 * a.q_sb2 + (long)lq * a.q_si + (long)(h0 + h) * D + d);
       qf[i][kc] = __builtin_bit_cast(bf16x8, v);
     }
   }
@@ -899,8 +904,8 @@ __global__ void __launch_bounds__(256) attn_seqm_kernel(AttnArgs a, int H, int n
     const int j = i / cpr, c8 = (i - j * cpr) * 8;
     uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
     if (j < F) {
-      kv = *(const uint4*)(a.k + b1 * a.k_sb1 + b2 * a.k_sb2 + (long)j * a.k_si + c8);
-      vv = *(const uint4*)(a.v + b1 * a.v_sb1 + b2 * a.v_sb2 + (long)j * a.v_si + c8);
+      kv = *(const uint4*)(a.k + b1 * a.k_sb1 + b2 * a.k_sb2 + (long)j * a.k_si + h0 * D + c8);
+      vv = *(const uint4*)(a.v + b1 * a.v_sb1 + b2 * a.v_sb2 + (long)j * a.v_si + h0 * D + c8);
     }
     *(uint4*)(Ks + j * P + c8) = kv;
     *(uint4*)(Vs + j * P + c8) = vv;
@@ -908,11 +913,11 @@ __global__ void __launch_bounds__(256) attn_seqm_kernel(AttnArgs a, int H, int n
   __syncthreads();
 
   const int qq = lq >> 2, pp = lq & 3;
-  u16* ob = a.o + b1 * a.o_sb1 + b2 * a.o_sb2 + (long)lq * a.o_si;
+  u16* ob = a.o + b1 * a.o_sb1 + b2 * a.o_sb2 + (long)lq * a.o_si + (long)h0 * D;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int h = wid + 4 * i;
-    if (h >= H) break;
+    if (h >= HB) break;
     // s[r] = score(key 4 lg + r, query lq)
     f32x4 s = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -951,10 +956,18 @@ __global__ void __launch_bounds__(256) attn_seqm_kernel(AttnArgs a, int H, int n
   }
 }
 
-template <int D>
+template <int D, int HS = 1>
 static int launch_seqm(const AttnArgs& a, int batch, int heads, hipStream_t s) {
-  const size_t shm = (size_t)2 * 16 * (heads * D + 8) * sizeof(u16);
-  attn_seqm_kernel<D><<<batch, 256, shm, s>>>(a, heads, batch);
+  const size_t shm = (size_t)2 * 16 * (heads / HS * D + 8) * sizeof(u16);
+  if (shm > 64 * 1024) {
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute((const void*)attn_seqm_kernel<D, HS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)shm);
+      attr_set = true;
+    }
+  }
+  attn_seqm_kernel<D, HS><<<dim3(batch, HS), 256, shm, s>>>(a, heads, batch);
   return check_launch("attn_seqm_kernel");
 }
 
@@ -1362,6 +1375,7 @@ using namespace ls;
 static bool g_attn_v1 = getenv("LS_ATTN_V1") != nullptr;  // A/B switch: force the 16-query kernel
 static bool g_attn_v3 = getenv("LS_ATTN_V3") != nullptr;  // A/B switch: attn3 for d = 40 too
 static bool g_seq_valu = getenv("LS_ATTN_SEQ_VALU") != nullptr;  // A/B switch: dot-product short-sequence kernel
+static bool g_seq160_valu = getenv("LS_ATTN_SEQ160_VALU") != nullptr;  // A/B switch: ... for d = 160 only
 
 static AttnArgs attn_args(const ls_attn_desc* d) {
   AttnArgs a;
@@ -1437,8 +1451,13 @@ extern "C" int ls_attention(const ls_attn_desc* d, void* stream) {
                          (((uintptr_t)d->q | (uintptr_t)d->k | (uintptr_t)d->v | (uintptr_t)d->o) & 15) == 0;
     if (!g_attn_v1 && d->nq == d->nk && d->nk <= 16 && heads_packed && aligned && D % 40 == 0 &&
         (TS == 1 || TS == 2 || TS == 4) && H * 16 * TS <= 512 && 512 % (H * 16 * TS) == 0) {
-      if (!g_seq_valu && (D == 40 || D == 80) && H <= 8)
-        return D == 40 ? launch_seqm<40>(a, d->batch, H, s) : launch_seqm<80>(a, d->batch, H, s);
+      // heads split over 2 blocks at d = 80 (20 KB of LDS per block: 146 -> 142 us at 32 windows)
+      // and d = 160 (41 KB: 111 -> 83 us); d = 40 keeps all heads in one block (295 vs 340 us)
+      if (!g_seq_valu && D == 40 && H <= 8) return launch_seqm<40>(a, d->batch, H, s);
+      if (!g_seq_valu && D == 80 && H <= 8)
+        return H % 2 == 0 ? launch_seqm<80, 2>(a, d->batch, H, s) : launch_seqm<80>(a, d->batch, H, s);
+      if (!g_seq_valu && !g_seq160_valu && D == 160 && H <= 8 && H % 2 == 0)
+        return launch_seqm<160, 2>(a, d->batch, H, s);
       // 256-thread blocks (several per CU desynchronise the load and compute phases)
       // wherever one (sequence, head) set fits
       const bool small_blk = H * 16 * TS <= 256 && 256 % (H * 16 * TS) == 0;

@@ -11,6 +11,8 @@ CASES = [  # name, batch(frames), tokens, keys, heads, d, kind
     ("spatial L2 d160", 16 * W, 64, 64, 8, 160, "self"), ("cross L0 d40", 16 * W, 1024, 50, 8, 40, "cross"),
     ("cross L1 d80", 16 * W, 256, 50, 8, 80, "cross"), ("temporal L0 d40", W, 1024, 16, 8, 40, "temporal"),
     ("temporal L1 d80", W, 256, 16, 8, 80, "temporal"),
+    ("cross L2 d160", 16 * W, 64, 50, 8, 160, "cross"), ("cross L3 d160", 16 * W, 16, 50, 8, 160, "cross"),
+    ("spatial L3 d160", 16 * W, 16, 16, 8, 160, "self"), ("temporal L2 d160", W, 64, 16, 8, 160, "temporal"),
 ]
 if os.environ.get("CFG4"):  # configs[4]: 64^2 latent (WINDOWS windows of 16 frames)
     CASES = [("c4 spatial L0 d40", 16 * W, 4096, 4096, 8, 40, "self"),
