@@ -204,8 +204,10 @@ __global__ void __launch_bounds__(256) attn_kernel(AttnArgs a) {
 //   * DSUM = D with D % 16 != 0 (d = 40): the row sum l comes out of the PV MFMA --
 //     V's padding column D is set to 1.0 once, so O^T row D accumulates sum_k p_k
 //     (of the same bf16 p the numerator uses) and the 16 adds per score row go away.
-template <int KC, int ND, int DSUM>
-__global__ void __launch_bounds__(256, KC >= 5 ? 1 : 2) attn3_kernel(AttnArgs a) {
+// ONE: the key set fits one 64-key tile (the 50 audio tokens, the 8x8 / 4x4 levels' self
+// attention): a single LDS stage and no prefetch registers, so d = 160 runs two blocks per CU.
+template <int KC, int ND, int DSUM, bool ONE = false>
+__global__ void __launch_bounds__(256, (KC >= 5 && !ONE) ? 1 : 2) attn3_kernel(AttnArgs a) {
   constexpr int DP = KC * 32;
   constexpr int KT = 64;
   constexpr int PITCH = DP + 8;
@@ -230,7 +232,7 @@ __global__ void __launch_bounds__(256, KC >= 5 ? 1 : 2) attn3_kernel(AttnArgs a)
 
   // K d-padding zeroed in both buffers; with DSUM, V[:, DSUM] = 1 and the rest of the
   // padding 0 (the per-tile stores never touch chunks >= cpr)
-  for (int i = tid; i < 2 * KT; i += 256) {
+  for (int i = tid; i < (ONE ? 1 : 2) * KT; i += 256) {
     u16* krow = sm + (i / KT) * 2 * TILE + (i % KT) * PITCH;
     for (int c = cpr * 8; c < DP; c += 8) *(uint4*)(krow + c) = make_uint4(0, 0, 0, 0);
     if (DSUM) {
@@ -301,7 +303,7 @@ __global__ void __launch_bounds__(256, KC >= 5 ? 1 : 2) attn3_kernel(AttnArgs a)
     constexpr bool PARTIAL = decltype(partial_tag)::value;
     const int t0 = t * KT;
     __syncthreads();
-    if (t + 1 < ntile) gload(t0 + KT);
+    if (!ONE && t + 1 < ntile) gload(t0 + KT);
     const u16* Ks = sm + (t & 1) * 2 * TILE;
     const u16* Vs = Ks + TILE;
     // S^T - m = K Q^T + (-m): scores relative to the running max, log2 units
@@ -381,7 +383,7 @@ __global__ void __launch_bounds__(256, KC >= 5 ? 1 : 2) attn3_kernel(AttnArgs a)
         oacc[1][nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[1], oacc[1][nd], 0, 0, 0);
       }
     }
-    if (t + 1 < ntile) lstore((t + 1) & 1);
+    if (!ONE && t + 1 < ntile) lstore((t + 1) & 1);
   };
   const int nfull = a.nk / KT;
   for (int t = 0; t < nfull; ++t) tile(t, std::false_type{});
@@ -708,20 +710,28 @@ static int launch_attn5(const AttnArgs& a, int batch, int heads, hipStream_t s) 
   return check_launch("attn5_kernel");
 }
 
-template <int KC, int ND, int DSUM>
-static int launch_attn3(const AttnArgs& a, int batch, int heads, hipStream_t s) {
+template <int KC, int ND, int DSUM, bool ONE>
+static int launch_attn3_(const AttnArgs& a, int batch, int heads, hipStream_t s) {
   const dim3 grid(cdiv(a.nq, 128), heads, batch);
-  const size_t shm = 2 * 2 * (size_t)64 * (KC * 32 + 8) * sizeof(u16);
+  const size_t shm = (ONE ? 1 : 2) * 2 * (size_t)64 * (KC * 32 + 8) * sizeof(u16);
   if (shm > 64 * 1024) {
     static bool attr_set = false;
     if (!attr_set) {
-      hipFuncSetAttribute((const void*)attn3_kernel<KC, ND, DSUM>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)shm);
+      (void)hipFuncSetAttribute((const void*)attn3_kernel<KC, ND, DSUM, ONE>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
       attr_set = true;
     }
   }
-  attn3_kernel<KC, ND, DSUM><<<grid, 256, shm, s>>>(a);
+  attn3_kernel<KC, ND, DSUM, ONE><<<grid, 256, shm, s>>>(a);
   return check_launch("attn3_kernel");
+}
+
+static bool g_attn3_two = getenv("LS_ATTN3_TWO_STAGE") != nullptr;  // A/B switch: no single-tile variant
+
+template <int KC, int ND, int DSUM>
+static int launch_attn3(const AttnArgs& a, int batch, int heads, hipStream_t s) {
+  if (a.nk <= 64 && !g_attn3_two) return launch_attn3_<KC, ND, DSUM, true>(a, batch, heads, s);
+  return launch_attn3_<KC, ND, DSUM, false>(a, batch, heads, s);
 }
 
 template <int DP, int NKF>
