@@ -874,7 +874,7 @@ __global__ void __launch_bounds__(NT, 4) attn_seq_kernel(AttnArgs a, int H, int 
 // that is ~60 wave instructions where the dot-product kernel spends ~450, which
 // leaves the kernel bound by the q/k/v/o stream.
 // Host contract: nq == nk <= 16, heads <= 8 (two per wave), heads contiguous,
-// D in {40, 80, 160}, rows 8-element aligned (16-B loads, 8-B stores).  HS > 1 splits a
+// D in {40, 80, 160}, rows 8-element aligned (16-B loads and stores).  HS > 1 splits a
 // sequence's heads over HS blocks (blockIdx.y), each staging only its heads' channels:
 // d = 160 with all 8 heads would need 82 KB of LDS (one block per CU), 4 heads 41 KB.
 template <int D, int HS = 1>
@@ -955,13 +955,23 @@ __global__ void __launch_bounds__(256) attn_seqm_kernel(AttnArgs a, int H, int n
     }
     const float inv = 1.f / xor16_32_sum(l);
     const u16* va = Vs + (4 * lg + qq) * P + h * D + 4 * pp;
+    uint2 w[ND + 1];
 #pragma unroll
     for (int nd = 0; nd < ND; ++nd) {
       const v4i16 vt = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)(va + nd * 16));
       const f32x4 o = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vt, pb, (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      const int d = nd * 16 + 4 * lg;
-      if (lq < F && d < D)
-        *(uint2*)(ob + h * D + d) = make_uint2(pack2(o[0] * inv, o[1] * inv), pack2(o[2] * inv, o[3] * inv));
+      w[nd] = make_uint2(pack2(o[0] * inv, o[1] * inv), pack2(o[2] * inv, o[3] * inv));
+    }
+    w[ND] = make_uint2(0, 0);
+    // 16-B stores: fragments 2p and 2p+1 trade halves between lane groups (permlane16
+    // swap), so every lane holds 8 consecutive dims -- lane group g stores dims
+    // 32 p + 16 (g & 1) + 4 (g & 2) .. + 7 (8-B stores were store-issue bound)
+#pragma unroll
+    for (int p = 0; p < (ND + 1) / 2; ++p) {
+      const auto rx = __builtin_amdgcn_permlane16_swap(w[2 * p].x, w[2 * p + 1].x, false, false);
+      const auto ry = __builtin_amdgcn_permlane16_swap(w[2 * p].y, w[2 * p + 1].y, false, false);
+      const int d = 32 * p + 16 * (lg & 1) + 4 * (lg & 2);
+      if (lq < F && d < D) *(uint4*)(ob + h * D + d) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
     }
   }
 }
