@@ -37,6 +37,7 @@ struct AttnArgs {
   long o_sb1, o_sb2, o_si, o_sh;
   int z2, nq, nk, D;
   float scale_log2;
+  int o16;  // o rows and head slices 16-B aligned: epilogues may store 8 dims per lane
 };
 
 // up to 8 bf16 from a possibly unaligned address, zero beyond `n`
@@ -400,7 +401,23 @@ __global__ void __launch_bounds__(256, (KC >= 5 && !ONE) ? 1 : 2) attn3_kernel(A
     }
     const float inv = 1.f / lt;
     const int q = q0 + g * 16 + lq;
-    if (q < a.nq) {
+    if (ONE && a.o16 && a.D % 8 == 0) {
+      // 16-B stores: fragments 2p, 2p+1 trade halves across lane groups (as attn_seqm)
+      uint2 w[ND + 1];
+#pragma unroll
+      for (int nd = 0; nd < ND; ++nd)
+        w[nd] = make_uint2(pack2(oacc[g][nd][0] * inv, oacc[g][nd][1] * inv),
+                           pack2(oacc[g][nd][2] * inv, oacc[g][nd][3] * inv));
+      w[ND] = make_uint2(0, 0);
+      u16* orow = ob + (long)(q < a.nq ? q : 0) * a.o_si;
+#pragma unroll
+      for (int p = 0; p < (ND + 1) / 2; ++p) {
+        const auto rx = __builtin_amdgcn_permlane16_swap(w[2 * p].x, w[2 * p + 1].x, false, false);
+        const auto ry = __builtin_amdgcn_permlane16_swap(w[2 * p].y, w[2 * p + 1].y, false, false);
+        const int d = 32 * p + 16 * (lg & 1) + 4 * (lg & 2);
+        if (q < a.nq && d < a.D) *(uint4*)(orow + d) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+      }
+    } else if (q < a.nq) {
       u16* orow = ob + (long)q * a.o_si;
 #pragma unroll
       for (int nd = 0; nd < ND; ++nd) {
@@ -1406,6 +1423,8 @@ static AttnArgs attn_args(const ls_attn_desc* d) {
   a.o_sb1 = d->o_sb1; a.o_sb2 = d->o_sb2; a.o_si = d->o_si; a.o_sh = d->o_sh;
   a.z2 = d->z2; a.nq = d->nq; a.nk = d->nk; a.D = d->head_dim;
   a.scale_log2 = d->scale * 1.4426950408889634f;
+  a.o16 = ((uintptr_t)d->o & 15) == 0 && d->o_si % 8 == 0 && d->o_sh % 8 == 0 && d->o_sb1 % 8 == 0 &&
+          d->o_sb2 % 8 == 0;
   return a;
 }
 
