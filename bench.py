@@ -14,10 +14,11 @@ directly spawns N fresh worker processes of this script (RANK / LOCAL_RANK /
 WORLD_SIZE / MASTER_* in their environment) BEFORE anything touches the GPU and
 exits with the first failing worker's status; under torchrun the process is
 already a worker.  Every rank runs its own windows (weak scaling; rank r owns
-windows r, r+N, ... of the job) and the decoded uint8 frames of all ranks are
-all-gathered once at the end of the timed loop (RCCL over xGMI, the only
-collective; the process group carries a timeout so a dead rank aborts the
-gather instead of hanging it).  `n_gpus` is the world size the process group
+windows r, r+N, ... of the job) and the decoded frames of all ranks are
+all-gathered once at the end of the timed loop as the fp32 pasted frames
+LipsyncPipeline.run_windows exchanges (RCCL over xGMI, the only collective; the
+uint8 clip is derived after it; the process group carries a timeout so a dead
+rank aborts the gather instead of hanging it).  `n_gpus` is the world size the process group
 reports.  Rank 0 prints ONE JSON line.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1|2|4]
@@ -42,7 +43,7 @@ sys.path.insert(0, REPO)
 # importing these does not touch the GPU (the HIP library loads on first use)
 from latentsync_amd import ops  # noqa: E402
 from latentsync_amd import unet as U  # noqa: E402
-from latentsync_amd.pipeline import load_fixed_mask  # noqa: E402
+from latentsync_amd.pipeline import frames_to_u8, load_fixed_mask  # noqa: E402
 
 SCHED_CFG = dict(beta_end=0.012, beta_schedule="scaled_linear", beta_start=0.00085, clip_sample=False,
                  num_train_timesteps=1000, set_alpha_to_one=False, steps_offset=1)  # configs/scheduler_config.json
@@ -303,13 +304,15 @@ class PlumbingEngine:
 
     def __init__(self, F, R, nw, rank, world):
         self.F, self.R, self.nw, self.rank, self.world = F, R, nw, rank, world
-        self.out_u8 = torch.zeros((nw * F, R, R, 3), dtype=torch.uint8)
+        self.out = torch.zeros((nw * F, 3, R, R), dtype=torch.float32)
         self.calls = 0
 
     def run(self):
         for k in range(self.nw):
             local = self.calls * self.nw + k
-            self.out_u8[k * self.F:(k + 1) * self.F] = (self.rank + local * self.world) % 251
+            # window index w encoded as the pasted value whose uint8 is w % 251
+            w = (self.rank + local * self.world) % 251
+            self.out[k * self.F:(k + 1) * self.F] = (w + 0.5) / 255 * 2 - 1
         self.calls += 1
 
 
@@ -397,8 +400,9 @@ def worker(args):
 
     K, W = args.steps, args.warmup
     FB = F * nw  # frames per step (batch of windows)
-    # rank r owns windows r, r+N, ... of the job (shard.rank_windows); K*nw per rank
-    mine = torch.empty((K * nw, F, R, R, 3), dtype=torch.uint8, device=device)
+    # rank r owns windows r, r+N, ... of the job (shard.rank_windows); K*nw per rank,
+    # kept as the fp32 pasted frames LipsyncPipeline.run_windows gathers
+    mine = torch.empty((K * nw, F, 3, R, R), dtype=torch.float32, device=device)
     for _ in range(max(W, 1) if not (args.no_graphs or plumbing) else W):
         eng.run()
     if plumbing:
@@ -422,9 +426,11 @@ def worker(args):
         if not plumbing:
             e1.record(st)
             ev_step.append((e0, e1))
-        mine[k * nw:(k + 1) * nw].copy_(eng.out_u8.view(nw, F, R, R, 3))
-    # decoded frames of every rank back in clip order: ONE all-gather over xGMI, at the end
-    gathered = shard.gather_windows(mine, world * K * nw)
+        mine[k * nw:(k + 1) * nw].copy_(eng.out.view(nw, F, 3, R, R))
+    # decoded frames of every rank back in clip order: ONE all-gather over xGMI, at the
+    # end, then the uint8 clip -- exactly LipsyncPipeline.run_windows' exchange
+    gathered = frames_to_u8(shard.gather_windows(mine, world * K * nw).flatten(0, 1))
+    gathered = gathered.view(world * K * nw, F, R, R, 3)
     sync()
     if world > 1:
         dist.barrier()

@@ -204,8 +204,8 @@ int ls_attention(const ls_attn_desc* d, void* stream);
  * attention"; replaces the same SDPA call, attention.py:271): QK^T and the softmax as
  * ls_attention (bf16 MFMA, fp32), P and V in OCP e4m3 on the block-scaled MFMA
  * v_mfma_scale_f32_16x16x128_f8f6f4.  V is quantised by a pre-pass into `workspace`
- * with one e8m0 scale per (head dim, 32 keys) -- MX block scaling, block max mapped
- * into [128, 256); P (<= 2^8 by the kernel's rescale threshold) uses scale 1 and the
+ * with one e8m0 scale per (head dim, 128-key tile) -- block scaling, the tile's max
+ * mapped into [128, 256), the same scale for all four 32-key MX blocks of a tile; P (<= 2^8 by the kernel's rescale threshold) uses scale 1 and the
  * row sums come from the same e4m3 P.  Two launches (quantise, attend), capturable.
  * head_dim 40 or 80 (the UNet's 64^2 / 32^2 levels); q/k/v rows 16-B aligned, o rows 8-B aligned.
  * Workspace: ls_attention_fp8_workspace_bytes(d) (0 = unsupported head_dim), 16-B aligned;

@@ -1894,26 +1894,36 @@ static void launch_rowblock1(const ConvArgs& a, int grid, hipStream_t s) {
 static const int kRowblockInstances[] = {0, RB_LN, RB_LN | RB_RV, RB_RES, RB_LN | RB_RES, RB_LN | RB_GEGLU, RB_GEGLU,
                                          RB_STATS, RB_RES | RB_STATS, RB_RES | RB_GNCS, RB_AFF, RB_AFF | RB_STATS};
 
-// the row-block instance flags for this call, or -1 (sets a.ntm / a.ntn)
-static int rowblock_flags(ConvArgs& a) {
+// the row-block instance flags for this call, or -1; the row-block grid goes to
+// *ntm / *ntn only (the caller's tiled grid in a.ntm / a.ntn stays valid for a fallback)
+static int rowblock_flags(const ConvArgs& a, int* ntm_out, int* ntn_out) {
   const int bm = a.K == 320 ? 256 : 128;
   const int ntm = a.M / bm, nch = a.N / 32;
-  a.ntm = ntm;
-  a.ntn = std::max(1, std::min(nch, (256 + ntm - 1) / ntm));
-  if (a.stats_out && a.ntn != 1) return -1;  // fused statistics need whole rows per block
-  if (a.cs_out && (bm % CS_ROWS || a.ntn != 1)) return -1;
+  const int ntn = std::max(1, std::min(nch, (256 + ntm - 1) / ntm));
+  if (a.stats_out && ntn != 1) return -1;  // fused statistics need whole rows per block
+  if (a.cs_out && (bm % CS_ROWS || ntn != 1)) return -1;
   const int flags = (a.ln_mr ? RB_LN : 0) | (a.res ? RB_RES : 0) | (a.rowvec ? RB_RV : 0) |
                     (a.act == LS_ACT_GEGLU ? RB_GEGLU : 0) | (a.stats_out ? RB_STATS : 0) | (a.cs_out ? RB_GNCS : 0) |
                     (a.aff_scale ? RB_AFF : 0);
   for (int f : kRowblockInstances)
-    if (f == flags) return flags;
+    if (f == flags) {
+      *ntm_out = ntm;
+      *ntn_out = ntn;
+      return flags;
+    }
   return -1;
 }
 
-// returns false when no instance matches (the caller then uses the tiled kernels)
-static bool launch_rowblock(ConvArgs& a, hipStream_t s) {
-  const int flags = rowblock_flags(a);
-  const int grid = a.ntm * a.ntn;
+// returns false when no instance matches (the caller then uses the tiled kernels with
+// its own, untouched a.ntm / a.ntn)
+static bool launch_rowblock(const ConvArgs& a0, hipStream_t s) {
+  int ntm = 0, ntn = 0;
+  const int flags = rowblock_flags(a0, &ntm, &ntn);
+  if (flags < 0) return false;
+  ConvArgs a = a0;
+  a.ntm = ntm;
+  a.ntn = ntn;
+  const int grid = ntm * ntn;
   switch (flags) {
     case 0: launch_rowblock1<0>(a, grid, s); return true;
     case RB_LN: launch_rowblock1<RB_LN>(a, grid, s); return true;
@@ -2234,7 +2244,8 @@ extern "C" int ls_conv_path(const ls_conv_desc* d) {
   ConvArgs a; TileCfg t; int split;
   if (build_args(d, a, t, split) != LS_OK) return -1;
   a.cs_out = nullptr;  // (the column sums never change the path)
-  if (rowblock_ok(d, a) && rowblock_flags(a) >= 0) return 1;
+  int ntm, ntn;
+  if (rowblock_ok(d, a) && rowblock_flags(a, &ntm, &ntn) >= 0) return 1;
   return (a.aff_scale || g_force_regstage) ? 2 : 0;
 }
 

@@ -87,6 +87,15 @@ def read_video_frames(video_path):
     return fr
 
 
+def frames_to_u8(frames):
+    """(n,3,R,R) fp32 pasted frames in [-1,1] -> (n,R,R,3) uint8 with exactly the
+    paste-back kernel's rounding (clamp(x/2+0.5, 0, 1)*255, truncated; fp32 throughout,
+    x/2 is exact so no contraction can change it) -- the u8 of the gathered clip is
+    derived from the one fp32 all-gather instead of being gathered a second time."""
+    u = ((frames / 2 + 0.5).clamp_(0, 1) * 255).to(torch.uint8)
+    return u.permute(0, 2, 3, 1).contiguous()
+
+
 class WindowEngine:
     """Device-resident executor of one 16-frame window; see module docstring."""
 
@@ -221,7 +230,9 @@ class WindowEngine:
         for j in range(self.steps):
             step()
             if callback is not None and j % callback_steps == 0:
-                callback(j, self.scheduler.timesteps[j], self.latents())
+                # a copy, as the reference's step returns a fresh tensor (:562-568): the
+                # next replay overwrites the engine's state buffer in place
+                callback(j, self.scheduler.timesteps[j], self.latents().clone())
         dec()
         return self.out
 
@@ -333,8 +344,11 @@ class LipsyncPipeline:
                 res[i] = (eng.out[fs].clone(), eng.out_u8[fs].clone())
         if world == 1:
             return torch.cat([res[i][0] for i in mine]), torch.cat([res[i][1] for i in mine])
-        # one all-gather of equally sized slabs: a short window is zero-padded to
-        # num_frames for the exchange and the padding dropped after it
+        # ONE all-gather of equally sized fp32 slabs (restore_video needs the fp32 faces:
+        # the reference resizes before it rounds to uint8, :343-358); a short window is
+        # zero-padded to num_frames for the exchange and the padding dropped after it.
+        # The uint8 frames are derived from the gathered fp32 ones, bit-identical to the
+        # engine's own (frames_to_u8).
         F_, dev = num_frames, self.device
 
         def padded(t):
@@ -342,9 +356,8 @@ class LipsyncPipeline:
                 return t
             return torch.cat([t, t.new_zeros((F_ - t.shape[0],) + tuple(t.shape[1:]))])
         loc = torch.stack([padded(res[i][0]) for i in mine]) if mine else torch.empty((0, F_, 3, R, R), device=dev)
-        loc8 = torch.stack([padded(res[i][1]) for i in mine]) if mine else \
-            torch.empty((0, F_, R, R, 3), dtype=torch.uint8, device=dev)
-        return (shard.gather_windows(loc, n_inf).flatten(0, 1)[:n], shard.gather_windows(loc8, n_inf).flatten(0, 1)[:n])
+        out = shard.gather_windows(loc, n_inf).flatten(0, 1)[:n]
+        return out, frames_to_u8(out)
 
     def restore_video(self, faces, video_frames, boxes, affine_matrices):
         """:343-358 on the device (latentsync_amd/restore.py): every face of the clip
@@ -372,6 +385,16 @@ class LipsyncPipeline:
         ``faces_only=True`` (or a video_path that is not an array file) the
         lip-synced aligned faces are written instead and no warp-back happens."""
         from . import repeat as rep
+        # write_video's brightness restore (util.py write_video, :594) belongs to the video
+        # writer, which this build does not carry: refuse it rather than ignore it
+        if use_darken or brightness_factor != 1.0:
+            raise NotImplementedError("use_darken / brightness_factor: the video writer's brightness restore "
+                                      "is out of scope (SURVEY.md §8(f)3)")
+        # the reference casts to weight_dtype (fp16 on CUDA, scripts/inference.py:33-34); this
+        # path computes in bf16 storage / fp32 accumulation for either half type
+        if weight_dtype not in (torch.float16, torch.bfloat16):
+            raise NotImplementedError(f"weight_dtype {weight_dtype}: the MI355X path computes in bf16 "
+                                      "(torch.float16 or torch.bfloat16 accepted)")
         if eta != 0.0:
             raise NotImplementedError("eta > 0")
         if mask != "fix_mask":
@@ -381,8 +404,10 @@ class LipsyncPipeline:
         data = load_data_pth(data_path)
         faces, boxes, affine_matrices = data["faces"], list(data["boxes"]), list(data["affine_matrices"])
         # the original frames are read up front (:405) because they are repeated /
-        # truncated together with the faces, boxes and matrices below
-        video_frames = None if kwargs.get("faces_only") else read_video_frames(video_path)
+        # truncated together with the faces, boxes and matrices below; only rank 0
+        # restores and writes, so the other ranks never decode or hold them
+        rank0 = shard.world_and_rank()[1] == 0
+        video_frames = None if (kwargs.get("faces_only") or not rank0) else read_video_frames(video_path)
         R = height or faces.shape[-1]
         self.check_inputs(R, width or R, callback_steps)
         if faces.shape[-1] != R:
@@ -419,8 +444,8 @@ class LipsyncPipeline:
         chunks = torch.stack([c.to(self.device) for c in chunks])
         out, out_u8 = self.run_windows(faces, chunks, keep, num_frames, num_inference_steps, guidance_scale,
                                        generator, callback=callback, callback_steps=callback_steps)
-        if shard.world_and_rank()[1] != 0:
-            return None  # every rank holds the gathered clip; rank 0 restores and writes it
+        if not rank0:
+            return None  # rank 0 restores and writes the gathered clip
         frames_out = out_u8
         if video_frames is not None:
             frames_out = self.restore_video(out, video_frames, boxes, affine_matrices)

@@ -452,11 +452,13 @@ def prepare_pixels(faces_u8, mask):
 
 
 def pipeline_window(unet_sd, unet_cfg, vae_sd, faces_u8, mask, audio_chunks, init_latent, eps_masked, eps_ref,
-                    num_steps=20, guidance_scale=1.0):
+                    num_steps=20, guidance_scale=1.0, step_latents=None):
     """One 16-frame window of LipsyncPipeline.__call__ (lipsync_pipeline.py:500-575).
     faces_u8 (F,3,R,R); mask (R,R) 1=keep; audio_chunks (F,50,384);
     init_latent (1,4,1,h,w) repeated over frames (prepare_latents :182-196);
-    eps_* (F,4,h,w) the VAE posterior noise.  Returns decoded+pasted (F,3,R,R)."""
+    eps_* (F,4,h,w) the VAE posterior noise.  Returns decoded+pasted (F,3,R,R).
+    ``step_latents``: a list that receives the (1,4,F,h,w) latents after every DDIM
+    step -- what the reference hands its callback (:562-568)."""
     Fn = faces_u8.shape[0]
     cfg_on = guidance_scale > 1.0
     pix, masked, m = prepare_pixels(faces_u8, mask)
@@ -481,6 +483,8 @@ def pipeline_window(unet_sd, unet_cfg, vae_sd, faces_u8, mask, audio_chunks, ini
             u, a = eps.chunk(2)
             eps = u + guidance_scale * (a - u)
         lat = ddim_step(ac, eps, int(t), lat, num_steps)
+        if step_latents is not None:
+            step_latents.append(lat.clone())
     z = lat / sc                                                                 # decode_latents :145-149
     z = z[0].permute(1, 0, 2, 3)
     dec = vae_decode(vae_sd, z)

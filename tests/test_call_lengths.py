@@ -180,10 +180,30 @@ def test_force_video_length_short_last_window(tmp_path, models, monkeypatch):
 
 
 def test_callback_per_step(tmp_path, models, monkeypatch):
-    """callback(j, t, latents) after every DDIM step of every window (:564-568)."""
-    calls = []
-    _run(tmp_path, models, monkeypatch, 16, 0.3,
-         callback=lambda j, t, lat: calls.append((j, int(t), tuple(lat.shape))))
+    """callback(j, t, latents) after every DDIM step of every window (:564-568).
+    The latents a callback keeps must not change afterwards (the reference hands it
+    the fresh tensor scheduler.step returns) and must match the oracle's per-step
+    latents."""
+    from oracle import ref_cpu as R
+    calls, kept = [], []
+
+    def cb(j, t, lat):
+        calls.append((j, int(t), tuple(lat.shape)))
+        kept.append(lat)  # kept as handed over, not copied here
+    seen, _, (faces, _, _, _) = _run(tmp_path, models, monkeypatch, 16, 0.3, callback=cb)
     h = RR // 8
     # 0.3 s of audio -> 16 padded chunks -> 2 windows of 8 frames, 2 steps each
     assert calls == [(0, 501, (1, 4, FR, h, h)), (1, 1, (1, 4, FR, h, h))] * 2
+    assert not torch.equal(kept[0], kept[1]) and not torch.equal(kept[1], kept[3])
+    unet, vae, _ = models
+    monkeypatch.setitem(R.VAE_CFG, "block_out_channels", (32, 64, 64, 64))
+    for i, s in enumerate(seen["sizes"]):
+        sl = slice(i * FR, i * FR + s)
+        ref_steps = []
+        R.pipeline_window(unet.state_dict(), dict(unet.config), vae._sd, faces[sl], seen["mask"], seen["chunks"][sl],
+                          seen["init"], seen["noise"][i][0], seen["noise"][i][1], num_steps=STEPS,
+                          guidance_scale=1.0, step_latents=ref_steps)
+        for j in range(STEPS):
+            e = rel_err(kept[i * STEPS + j].float().cpu(), ref_steps[j])
+            print("window", i, "step", j, e)
+            assert e < 3e-2

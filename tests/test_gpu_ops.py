@@ -387,6 +387,23 @@ def test_rowblock_gemm(gpu, K, M, N, case):
     assert rel_err(y.float(), y_tiled.float()) < 1e-2
 
 
+@pytest.mark.parametrize("M", [512, 65536])
+def test_rowblock_uncompiled_flags_fall_back(gpu, M):
+    """A row-block-eligible shape (K = 320, 1x1) whose epilogue flags have no compiled
+    row-block instance (residual + row vector) must run on the tiled kernels with the
+    tiled grid, not the row-block grid (rowblock_flags overwrote ntm/ntn)."""
+    K, N, rpv = 320, 320, 256
+    x = bf(rnd(M, K, seed=97))
+    w = rnd(N, K, seed=98, scale=1 / math.sqrt(K))
+    b = rnd(N, seed=99, scale=0.1)
+    rv = rnd(M // rpv, N, seed=100)
+    res = bf(rnd(M, N, seed=101))
+    y = ops.linear(x.to(torch.bfloat16).to(DEV), packed(w, b, 1), res=res.to(torch.bfloat16).to(DEV),
+                   rowvec=(rv.to(DEV), rpv, N))
+    ref = x @ bf(w).T + b + rv.repeat_interleave(rpv, 0) + res
+    assert rel_err(y.float().cpu(), ref) < 1e-2
+
+
 @pytest.mark.parametrize("K,M,N,res", [(320, 65536, 320, True), (320, 8192, 320, False), (640, 4096, 640, False),
                                        (640, 4096, 640, True), (1280, 2048, 1280, True), (320, 512, 320, True)])
 def test_linear_row_stats_out(gpu, K, M, N, res):
@@ -452,6 +469,25 @@ def test_groupnorm_colsum_concat(gpu):
     sc, sh = ops.group_norm(xa, 32, 1e-6, gamma, beta, 2, x2=xb)
     sc2, sh2 = ops.group_norm(xa.clone(), 32, 1e-6, gamma, beta, 2, x2=xb.clone())
     assert rel_err(sc.cpu(), sc2.cpu()) < 1e-4 and rel_err(sh.cpu(), sh2.cpu()) < 1e-4
+
+
+@pytest.mark.parametrize("offset", [10.0, 30.0])
+def test_groupnorm_colsum_large_mean(gpu, offset):
+    """Column-sum statistics are raw fp32 slot sums (var = E[x^2] - mean^2 in fp64), so
+    their relative variance error is ~sqrt(128) eps32 (1 + mean^2 / var) -- here with
+    mean / std = 10 and 30 (VAE-decoder-like DC offsets) against the shifted read pass
+    and an fp64 reference: scale within 1e-3 (bf16 rounding of y is 3.9e-3)."""
+    n, H, C = 8, 32, 128
+    x = nhwc(bf(rnd(n, C, H, H, seed=74) + offset))
+    ops.gn_colsum(x)
+    gamma, beta = (1 + 0.1 * rnd(C, seed=75)).to(DEV), (0.1 * rnd(C, seed=76)).to(DEV)
+    sc, sh = ops.group_norm(x, 32, 1e-6, gamma, beta, 2)
+    sc2, sh2 = ops.group_norm(x.clone(), 32, 1e-6, gamma, beta, 2)
+    xd = x.double().cpu().reshape(2, -1, 32, C // 32)
+    var = xd.var(dim=(1, 3), unbiased=False)  # (sample, group)
+    ref = gamma.double().cpu().reshape(1, 32, -1) / (var + 1e-6).sqrt()[..., None]
+    assert rel_err(sc.cpu().double(), ref.reshape(2, C)) < 1e-3
+    assert rel_err(sc.cpu(), sc2.cpu()) < 1e-3 and rel_err(sh.cpu(), sh2.cpu()) < 1e-3
 
 
 @pytest.mark.parametrize("K,M,N,H,silu", [(320, 65536, 320, 32, False), (640, 32768, 640, 16, False),

@@ -128,3 +128,13 @@ def test_call_data_pth_with_restore(tmp_path, monkeypatch):
          num_frames=Fr, num_inference_steps=2, guidance_scale=1.0, data_path=str(tmp_path / "data.pth"),
          mask_image_path=None, faces_only=True)
     assert np.load(out_path)["frames"].shape == (n, Rr, Rr, 3)
+
+
+@pytest.mark.parametrize("kw", [dict(use_darken=True), dict(brightness_factor=1.2), dict(weight_dtype=torch.float32)])
+def test_call_refuses_unsupported_options(kw):
+    """Options whose effect this build does not reproduce raise instead of being
+    ignored: the writer's brightness restore (lipsync_pipeline.py:384-385, :594) and a
+    non-half weight_dtype (:374; this path computes in bf16)."""
+    pipe = LipsyncPipeline.__new__(LipsyncPipeline)
+    with pytest.raises(NotImplementedError):
+        pipe(video_path="v.npy", audio_path="a.wav", video_out_path="o.npz", data_path="d.pth", **kw)
