@@ -19,7 +19,6 @@ three captured hipGraphs replayed back to back --
 Random draws are injected (initial latent noise, VAE posterior noise), as the
 parity harness requires (SURVEY.md §7 "RNG").
 """
-import gc
 import math
 import os
 
@@ -96,6 +95,22 @@ def frames_to_u8(frames):
     return u.permute(0, 2, 3, 1).contiguous()
 
 
+# Graph lifetime.  A hipGraph must not be destroyed while a stream is capturing (the
+# runtime aborts), and an engine that becomes cyclic garbage can be collected at any
+# allocation -- including inside another engine's capture.  So an engine never
+# destroys its graphs itself: close() and __del__ only move them here (a list append,
+# no HIP call), and they are destroyed at the next safe point: the start of a capture
+# (before it begins), or release_retired_graphs() outside any capture.
+_RETIRED_GRAPHS = []
+
+
+def release_retired_graphs():
+    """Destroy the graphs of closed / collected engines, if no stream is capturing."""
+    if _RETIRED_GRAPHS and not torch.cuda.is_current_stream_capturing():
+        while _RETIRED_GRAPHS:
+            _RETIRED_GRAPHS.pop().reset()
+
+
 class WindowEngine:
     """Device-resident executor of one 16-frame window; see module docstring."""
 
@@ -164,29 +179,44 @@ class WindowEngine:
         ops.paste_back(dec, self.pix, self.mask, self.out, self.out_u8)
 
     def capture(self):
-        """Warm up eagerly once, then capture the three phases as hipGraphs."""
+        """Warm up eagerly once, then capture the three phases as hipGraphs.  Graphs
+        of engines closed or collected earlier are destroyed first, outside the
+        capture; an engine collected DURING the capture only retires its graphs."""
         self._encode()
         self._step()
         self._decode()
         torch.cuda.synchronize(self.device)
+        self._retire()
+        release_retired_graphs()
         pool = torch.cuda.graph_pool_handle()
         graphs = []
-        # no garbage collection while a stream is capturing: a collected engine's graphs
-        # would be destroyed mid-capture, which aborts the HIP runtime (torch.cuda.graph
-        # collects once on entry; the host code inside can create new cyclic garbage)
-        gc_was_on = gc.isenabled()
-        gc.disable()
         try:
             for fn in (self._encode, self._step, self._decode):
                 g = torch.cuda.CUDAGraph()
+                graphs.append(g)
                 with torch.cuda.graph(g, pool=pool):
                     fn()
-                graphs.append(g)
-        finally:
-            if gc_was_on:
-                gc.enable()
+        except BaseException:
+            _RETIRED_GRAPHS.extend(graphs)
+            raise
         torch.cuda.synchronize(self.device)
         self.graphs = graphs
+
+    def _retire(self):
+        g = self.__dict__.get("graphs")
+        if g:
+            _RETIRED_GRAPHS.extend(g)
+        self.graphs = None
+
+    def close(self):
+        """Release the captured graphs now (deferred if a stream is capturing).  The
+        engine stays usable: the next run() captures again."""
+        self._retire()
+        release_retired_graphs()
+
+    def __del__(self):
+        # may run inside another engine's capture (cyclic GC): no HIP call here
+        self._retire()
 
     # -- inputs / execution -------------------------------------------------------
     def load(self, faces_u8, mask, audio_chunks, init_latent, eps_masked, eps_ref):
@@ -278,10 +308,21 @@ class LipsyncPipeline:
 
     def engine(self, num_frames, resolution, steps, guidance_scale, use_graphs=True, windows=1):
         key = (num_frames, resolution, steps, float(guidance_scale), use_graphs, windows)
-        if key not in self._engines:
-            self._engines[key] = WindowEngine(self.denoising_unet, self.vae, self.scheduler, num_frames, resolution,
-                                              steps, guidance_scale, use_graphs, windows=windows)
-        return self._engines[key]
+        eng = self._engines.get(key)
+        if eng is not None and (eng.unet is not self.denoising_unet or eng.ud is not self.denoising_unet._dev or
+                                eng.vae is not self.vae or eng.scheduler is not self.scheduler):
+            eng.close()  # the models were swapped or re-packed: this engine is stale
+            eng = None
+        if eng is None:
+            eng = self._engines[key] = WindowEngine(self.denoising_unet, self.vae, self.scheduler, num_frames,
+                                                    resolution, steps, guidance_scale, use_graphs, windows=windows)
+        return eng
+
+    def close(self):
+        """Release every cached window engine and its graphs deterministically."""
+        for eng in self._engines.values():
+            eng.close()
+        self._engines.clear()
 
     def prepare_latents(self, num_frames, height, width, generator=None):
         """:182-196 -- one (1,4,1,h,w) draw repeated over every frame."""

@@ -142,3 +142,49 @@ def test_window_configs4_shape(gpu, monkeypatch):
     e = rel_err(out, ref)
     print("configs[4]-shape window rel_err", e)
     assert e < 3e-2
+
+
+def test_engines_dropped_during_capture(gpu):
+    """Graph lifetime (round-2 abort, commit ee7a273): engines are built, captured and
+    dropped back to back, one of them as unreachable cyclic garbage that the collector
+    frees INSIDE the next engine's capture.  Its graphs are only retired there (no HIP
+    call mid-capture) and destroyed at the next safe point; nothing depends on the
+    collector being off.  The captured engine still matches its eager run."""
+    import gc
+
+    from latentsync_amd import pipeline as P
+    Fr, Rr, steps = 4, 64, 2
+    h = Rr // 8
+    unet = UNet3DConditionModel(**TINY_MODEL).init_weights(9).to("cuda").eval()
+    vae = AutoencoderKL(block_out_channels=(32, 64, 64, 64)).init_weights(10).to("cuda")
+    g = torch.Generator().manual_seed(11)
+    inp = [(torch.rand((Fr, 3, Rr, Rr), generator=g) * 255).to(torch.uint8), load_fixed_mask(Rr),
+           torch.randn((Fr, 50, 384), generator=g), torch.randn((1, 4, 1, h, h), generator=g),
+           torch.randn((Fr, 4, h, h), generator=g), torch.randn((Fr, 4, h, h), generator=g)]
+    inp = [t.cuda() for t in inp]
+    assert gc.isenabled()
+    for it in range(3):
+        dead = WindowEngine(unet, vae, DDIMScheduler(**SCHED), Fr, Rr, steps, 1.0)
+        dead.load(*inp)
+        dead.run()
+        dead.cycle = dead  # unreachable after `del`, freed only by the collector
+        del dead
+        eng = WindowEngine(unet, vae, DDIMScheduler(**SCHED), Fr, Rr, steps, 1.0)
+        real_step = eng._step
+
+        def step_with_gc():
+            if torch.cuda.is_current_stream_capturing():
+                gc.collect()  # frees `dead` while the step graph is being captured
+            real_step()
+        eng._step = step_with_gc
+        eng.load(*inp)
+        out = eng.run().cpu()
+        assert P._RETIRED_GRAPHS, "the collected engine's graphs were not retired"
+        eager = WindowEngine(unet, vae, DDIMScheduler(**SCHED), Fr, Rr, steps, 1.0, use_graphs=False)
+        eager.load(*inp)
+        assert rel_err(out, eager.run().cpu()) < 1e-3
+        eng.close()  # outside capture: retired graphs are destroyed now
+        assert not P._RETIRED_GRAPHS and eng.graphs is None
+        out2 = eng.run().cpu()  # a closed engine captures again
+        assert torch.equal(out, out2)
+        eng.close()

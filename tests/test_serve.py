@@ -1,0 +1,192 @@
+"""The HTTP job server (latentsync_amd/serve.py; reference scripts/api.py:21-219) on
+CPU with FastAPI's TestClient and stand-in pipelines: the endpoints and wire format,
+the per-request file layout, the reference's pipeline arguments, error propagation
+(400 for missing inputs, other failures to the waiting request), the bounded queue's
+"Queue is full" reply, and dispatch over one worker per GPU (each strictly one
+request at a time)."""
+import asyncio
+import os
+import threading
+import time
+
+import pytest
+from fastapi.testclient import TestClient
+
+from latentsync_amd import serve as S
+
+
+class StubPipeline:
+    """Records each call and writes an output file, as the real __call__ does."""
+
+    def __init__(self, delay=0.0, fail=None, gate=None):
+        self.calls, self.delay, self.fail, self.gate = [], delay, fail, gate
+        self.active = 0
+        self.max_active = 0
+        self.lock = threading.Lock()
+
+    def __call__(self, **kw):
+        with self.lock:
+            self.active += 1
+            self.max_active = max(self.max_active, self.active)
+        try:
+            if self.gate is not None:
+                self.gate.wait(30)
+            time.sleep(self.delay)
+            self.calls.append(kw)
+            if self.fail:
+                raise RuntimeError(self.fail)
+            open(kw["video_out_path"], "wb").close()
+        finally:
+            with self.lock:
+                self.active -= 1
+
+
+def _files(d, vid="v1", rid="r1", darken=False, rotated=False):
+    suf = "_rotated" if rotated else ""
+    names = [f"{vid}.mp4", f"{vid}.pth", f"{rid}.wav"]
+    if rotated:
+        names += [f"{vid}_rotated.mp4", f"{vid}_rotated.pth"]
+    if darken:
+        names += [f"{vid}_darken{suf}.mp4", f"{vid}_darken{suf}.pth"]
+    for n in names:
+        open(os.path.join(d, n), "wb").close()
+
+
+def _client(tmp_path, pipes, queue_size=10):
+    kw = dict(data_dir=str(tmp_path), results_dir=str(tmp_path / "results"), resolution=256)
+    app = S.create_app([S.InlineWorker(p, rank=i, **kw) for i, p in enumerate(pipes)], queue_size=queue_size)
+    return app, TestClient(app)
+
+
+def test_ping_and_process(tmp_path):
+    _files(tmp_path)
+    pipe = StubPipeline()
+    app, c = _client(tmp_path, [pipe])
+    with c:
+        assert c.get("/ping").json() == {"message": "pong"}
+        r = c.post("/process", json={"id": "r1", "video_id": "v1", "audio_url": "unused"})
+        assert r.status_code == 200
+        body = r.json()
+    assert body["message"] == "Request processed successfully" and body["gif_url"] is None
+    assert body["output_url"] == str(tmp_path / "results" / "r1.npz") and os.path.exists(body["output_url"])
+    assert body["elapsed_time"] >= 0
+    kw = pipe.calls[0]
+    # the reference's pipeline arguments (api.py:138-154)
+    assert kw["video_path"] == str(tmp_path / "v1.mp4") and kw["data_path"] == str(tmp_path / "v1.pth")
+    assert kw["audio_path"] == str(tmp_path / "r1.wav")
+    assert (kw["num_frames"], kw["num_inference_steps"], kw["guidance_scale"]) == (16, 20, 1.5)
+    assert (kw["width"], kw["height"], kw["start_from_backwards"], kw["force_video_length"]) == (256, 256, False, False)
+    assert (kw["use_darken"], kw["brightness_factor"]) == (False, 1.0)
+
+
+def test_path_rules(tmp_path):
+    """api.py:103-123: rotated clip for dynamic clips when both files exist, darkened
+    variants, and the audio fetched from a local path when missing."""
+    _files(tmp_path, darken=True, rotated=True)
+    p = {"id": "r2", "video_id": "v1", "is_dynamic_clip": True, "use_darken": True}
+    v, d, a = S.resolve_paths(p, str(tmp_path))
+    assert v.endswith("v1_darken_rotated.mp4") and d.endswith("v1_darken_rotated.pth") and a.endswith("r2.wav")
+    v, d, _ = S.resolve_paths(dict(p, is_dynamic_clip=False), str(tmp_path))
+    assert v.endswith("v1_darken.mp4") and d.endswith("v1_darken.pth")
+    v, d, _ = S.resolve_paths(dict(p, use_darken=False), str(tmp_path))
+    assert v.endswith("v1_rotated.mp4")
+    src = tmp_path / "src.wav"
+    src.write_bytes(b"RIFF")
+    pipe = StubPipeline()
+    _, c = _client(tmp_path, [pipe])
+    with c:
+        r = c.post("/process", json={"id": "r9", "video_id": "v1", "audio_url": "file://" + str(src)})
+    assert r.status_code == 200 and (tmp_path / "r9.wav").read_bytes() == b"RIFF"
+    assert S.calculate_inverse_factor(0.8) == 1.25 and S.calculate_inverse_factor(1.3) == 1.0
+
+
+def test_errors_propagate(tmp_path):
+    _files(tmp_path)
+    _, c = _client(tmp_path, [StubPipeline(fail="boom in the pipeline")])
+    with c:
+        r = c.post("/process", json={"id": "r1", "video_id": "missing", "audio_url": "x"})
+        assert r.status_code == 400 and r.json()["detail"] == "Video file not found."
+        r = c.post("/process", json={"id": "nowav", "video_id": "v1", "audio_url": "https://example.com/a.wav"})
+        assert r.status_code == 400 and r.json()["detail"] == "Audio file not found."
+        with pytest.raises(RuntimeError, match="boom in the pipeline"):
+            c.post("/process", json={"id": "r1", "video_id": "v1", "audio_url": "x"})
+        # the worker survives a failed request
+        assert c.get("/ping").status_code == 200
+
+
+def _run_dispatch(workers, payloads, queue_size):
+    async def go():
+        d = S.Dispatcher(workers, queue_size)
+        await d.start()
+        try:
+            res = await asyncio.gather(*[d.submit(p) for p in payloads], return_exceptions=True)
+        finally:
+            await d.stop()
+        return d, res
+    return asyncio.run(go())
+
+
+def test_queue_full(tmp_path):
+    """api.py:203-204: with the workers busy and the queue at maxsize, the next
+    request gets the 'Queue is full' reply instead of waiting."""
+    _files(tmp_path)
+    gate = threading.Event()
+    pipe = StubPipeline(gate=gate)
+    kw = dict(data_dir=str(tmp_path), results_dir=str(tmp_path / "results"))
+    w = S.InlineWorker(pipe, **kw)
+
+    async def go():
+        d = S.Dispatcher([w], queue_size=2)
+        await d.start()
+        first = []
+        for i in range(3):
+            first.append(asyncio.create_task(d.submit({"id": f"r{i}", "video_id": "v1", "audio_url": "x"})))
+            await asyncio.sleep(0.2)  # r0 taken by the worker (held by the gate), then r1, r2 queued
+        full = await d.submit({"id": "r1", "video_id": "v1", "audio_url": "x"})
+        gate.set()
+        done = await asyncio.gather(*first)
+        await d.stop()
+        return full, done
+    _files(tmp_path, rid="r0")
+    _files(tmp_path, rid="r2")
+    full, done = asyncio.run(go())
+    assert full is None and all(r["message"].startswith("Request processed") for r in done)
+
+
+def test_dispatch_one_request_per_gpu_worker(tmp_path):
+    """Requests spread over the per-GPU workers (up to N in flight), while each worker
+    runs strictly one at a time (its pipeline is not re-entrant)."""
+    pipes = [StubPipeline(delay=0.2) for _ in range(3)]
+    kw = dict(data_dir=str(tmp_path), results_dir=str(tmp_path / "results"))
+    for i in range(9):
+        _files(tmp_path, rid=f"q{i}")
+    t0 = time.time()
+    d, res = _run_dispatch([S.InlineWorker(p, rank=i, **kw) for i, p in enumerate(pipes)],
+                           [{"id": f"q{i}", "video_id": "v1", "audio_url": "x"} for i in range(9)], queue_size=10)
+    wall = time.time() - t0
+    assert all(isinstance(r, dict) for r in res), res
+    assert sorted(d.served.values()) == [3, 3, 3] or sum(d.served.values()) == 9
+    assert all(p.max_active == 1 for p in pipes)
+    assert all(len(p.calls) >= 1 for p in pipes)
+    assert wall < 9 * 0.2  # concurrent across workers, not serialised behind one semaphore
+
+
+def _stub_factory(rank):
+    return StubPipeline()
+
+
+def test_process_worker_spawns_pipeline_process(tmp_path):
+    """The per-GPU worker process: builds its pipeline from a factory, serves requests
+    over a pipe, maps HTTPException / other errors back to the server."""
+    _files(tmp_path)
+    w = S.ProcessWorker(0, "test_serve:_stub_factory", data_dir=str(tmp_path), results_dir=str(tmp_path / "res"))
+    w.start()
+    try:
+        res = asyncio.run(w.run({"id": "r1", "video_id": "v1", "audio_url": "x"}))
+        assert res["output_url"].endswith("r1.npz") and os.path.exists(res["output_url"])
+        with pytest.raises(S.HTTPException) as ei:
+            asyncio.run(w.run({"id": "r1", "video_id": "nope", "audio_url": "x"}))
+        assert ei.value.status_code == 400
+    finally:
+        w.stop()
+    assert not w.proc.is_alive()
