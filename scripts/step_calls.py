@@ -30,6 +30,7 @@ def main():
     eng = WindowEngine(unet, vae, DDIMScheduler(**bench.SCHED_CFG), 16, R, 20, 1.0, use_graphs=False, windows=nw)
     faces, audio, init, em, er = bench.synthetic_window(16 * nw, R, R // 8, 384, 1000, dev)
     eng.load(faces, load_fixed_mask(R).to(dev), audio, init, em, er)
+    eng._encode()
     eng._step()
     torch.cuda.synchronize()
     recs = []

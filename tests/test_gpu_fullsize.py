@@ -147,3 +147,45 @@ def test_configs4_window(vae, unet_full, precision):
     print(f"configs[4] window rel_err ({precision} attention)", e)
     assert e < 3e-2
     _pixel_check(out, ref, (mask < 1)[None, None])
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("guidance,Fr,steps", [(1.0, 16, 20), (2.0, 4, 20)])
+def test_headline_depth_window(vae, unet_full, guidance, Fr, steps):
+    """Parity at the headline depth: configs[1] exactly (stage2 UNet + full VAE, 256^2,
+    16 frames, 20 DDIM steps, guidance 1.0) and a CFG window (guidance 2.0, 20 steps,
+    4 frames: both UNet halves every step) through the graph-captured engine, against
+    oracle.pipeline_window in fp32 -- the bf16 error accumulated over 20 chained
+    UNet forwards, not just 2.  Same bounds as the 2-step windows; the measured rel-L2
+    and per-pixel max / p99.9 are printed."""
+    from latentsync_amd.pipeline import WindowEngine, load_fixed_mask
+    from latentsync_amd.scheduler import DDIMScheduler
+    from oracle import ref_cpu as O
+    torch.set_num_threads(16)
+    R = 256
+    h = R // 8
+    g = torch.Generator().manual_seed(21)
+    low = torch.rand((Fr, 3, R // 16, R // 16), generator=g)
+    faces = (torch.nn.functional.interpolate(low, size=(R, R), mode="bilinear") * 255).round().to(torch.uint8)
+    mask = load_fixed_mask(R)
+    audio = torch.randn((Fr, 50, 384), generator=g)
+    init = torch.randn((1, 4, 1, h, h), generator=torch.Generator().manual_seed(1247))
+    em, er = torch.randn((Fr, 4, h, h), generator=g), torch.randn((Fr, 4, h, h), generator=g)
+    eng = WindowEngine(unet_full, vae, DDIMScheduler(**SCHED), Fr, R, steps, guidance)
+    eng.load(faces.cuda(), mask.cuda(), audio.cuda(), init.cuda(), em.cuda(), er.cuda())
+    steps_gpu = []
+    out = eng.run(callback=lambda j, t, lat: steps_gpu.append(lat.float().cpu())).float().cpu()
+    steps_ref = []
+    with torch.no_grad():
+        ref = O.pipeline_window(unet_full.state_dict(), dict(unet_full.config), vae._sd, faces, mask, audio, init,
+                                em, er, num_steps=steps, guidance_scale=guidance, step_latents=steps_ref)
+    lat_errs = [rel_err(a, b) for a, b in zip(steps_gpu, steps_ref)]
+    print(f"headline-depth window g={guidance} F={Fr}: latent rel_err per step "
+          + " ".join(f"{x:.4f}" for x in lat_errs))
+    e = rel_err(out, ref)
+    print(f"headline-depth window g={guidance} F={Fr} steps={steps}: decoded rel_err {e:.4f}")
+    assert len(lat_errs) == steps and max(lat_errs) < 3e-2
+    assert e < 3e-2
+    _pixel_check(out, ref, (mask < 1)[None, None])
+    keep = (mask == 1)[None, None].expand_as(out)
+    assert int((_u8(out) - _u8(ref)).abs()[keep].max()) <= 1
