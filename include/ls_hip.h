@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LS_ABI_VERSION 8
+#define LS_ABI_VERSION 9
 
 typedef enum {
   LS_OK = 0,
@@ -213,6 +213,34 @@ int ls_attention(const ls_attn_desc* d, void* stream);
  */
 size_t ls_attention_fp8_workspace_bytes(const ls_attn_desc* d);
 int ls_attention_fp8(const ls_attn_desc* d, void* workspace, size_t workspace_bytes, void* stream);
+
+/*
+ * The motion module's temporal self-attention fused with its input side: replaces, per
+ * VersatileAttention block (latentsync/models/motion_module.py:203-218 and :262-313),
+ *   LayerNorm(h) -> "(b f) s c -> (b s) f c" + pe[:f] -> to_q / to_k / to_v -> SDPA over
+ *   the f frames (8 heads) -> "(b s) f c -> (b f) s c"
+ * writing the attention output o (before to_out).  The q|k|v projections never reach HBM.
+ *   x, o   : (n_samples * F * S) rows of C bf16, row (b*F + f)*S + s, pitches ldx / ldo
+ *   gamma  : fp32 [C], the LayerNorm weight;  bpe: fp32 [16][C], LayerNorm bias + pe row f
+ *   w      : bf16 [3C][C] packed per 80-column group g and 16-channel tile t = 0..4: q rows
+ *            80g+16t..+15 scaled by log2(e)/sqrt(C/8), then the same k rows, then v rows
+ *            (latentsync_amd/ops.py pack_temporal)
+ * C = 320 (d 40) or 640 (d 80), heads = 8, 1 <= F <= 16, S % 16 == 0 (C = 320) or S % 8 == 0
+ * (C = 640), 16-B aligned pointers, pitches % 8 == 0.
+ */
+typedef struct {
+  const uint16_t* x;
+  int32_t ldx;
+  const float* gamma;
+  const float* bpe;
+  const uint16_t* w;
+  uint16_t* o;
+  int32_t ldo;
+  int32_t C, heads, n_samples, F, S;
+  float eps;
+} ls_tattn_desc;
+
+int ls_temporal_attention(const ls_tattn_desc* d, void* stream);
 
 /*
  * Small-M linear in fp32: y[m, n] = sum_k act(x[m, k]) * W[n, k] + bias[n]

@@ -10,7 +10,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LS_HIP_LIB", os.path.join(HERE, "libls_hip.so"))
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 c_u16p = C.c_void_p
 c_vp = C.c_void_p
@@ -48,6 +48,12 @@ class AttnDesc(C.Structure):
     ]
 
 
+class TAttnDesc(C.Structure):
+    _fields_ = [("x", c_vp), ("ldx", C.c_int32), ("gamma", c_vp), ("bpe", c_vp), ("w", c_vp), ("o", c_vp),
+                ("ldo", C.c_int32), ("C", C.c_int32), ("heads", C.c_int32), ("n_samples", C.c_int32),
+                ("F", C.c_int32), ("S", C.c_int32), ("eps", C.c_float)]
+
+
 _SIGS = {
     "ls_abi_version": (C.c_int, []),
     "ls_last_error": (C.c_char_p, []),
@@ -68,6 +74,7 @@ _SIGS = {
     "ls_attention": (C.c_int, [C.POINTER(AttnDesc), c_vp]),
     "ls_attention_fp8_workspace_bytes": (C.c_size_t, [C.POINTER(AttnDesc)]),
     "ls_attention_fp8": (C.c_int, [C.POINTER(AttnDesc), c_vp, C.c_size_t, c_vp]),
+    "ls_temporal_attention": (C.c_int, [C.POINTER(TAttnDesc), c_vp]),
     "ls_small_linear": (C.c_int, [c_vp, C.c_int32, C.c_int32, c_vp, c_vp, C.c_int32, C.c_int32, c_vp, c_vp]),
     "ls_timestep_embed": (C.c_int, [c_vp, c_vp, C.c_int32, C.c_int32, C.c_int32, C.c_float, c_vp, c_vp]),
     "ls_ddim_cfg_step": (C.c_int, [c_vp, C.c_int32, C.c_int32, C.c_int64, C.c_float, c_vp, c_vp, c_vp, c_vp,

@@ -112,6 +112,27 @@ __device__ __forceinline__ float xor16_32_sum(float v) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
+// 16 B per lane global -> LDS DMA (global_load_lds_dwordx4): the wave-instruction
+// writes 64 consecutive 16-B slots from lds_dst (lane-linear), each lane's own source
+__device__ __forceinline__ void glds16(const void* src, uint4* lds_dst) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+
+template <int N> __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// LDS image of one operand tile: rows of BK bf16, 16-B chunks XOR-swizzled so
+// the 16-lane groups of a ds_read_b128 fragment read hit distinct bank slots.
+template <int BK>
+__device__ __forceinline__ int swz_bk(int row, int c) {
+  if (BK == 64) return row * 8 + (c ^ ((row >> 1) & 7));
+  return row * 4 + (c ^ ((-(row >> 2)) & 3));
+}
+
+__device__ __forceinline__ void load8f(const float* __restrict__ p, float* d) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+}
+
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 }  // namespace ls

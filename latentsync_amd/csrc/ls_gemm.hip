@@ -41,10 +41,6 @@ struct ConvArgs {
 // stores).  All global loads of a chunk are issued before its stores.
 struct Chunk8 { float v[8]; };
 
-__device__ __forceinline__ void load8f(const float* __restrict__ p, float* d) {
-  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
-  d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
-}
 
 __device__ __forceinline__ float act_fn(int act, float v) {
   if (act == LS_ACT_GELU) return gelu_erf(v);
@@ -578,9 +574,6 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvArgs a) {
 // k's MFMAs; counted vmcnt + raw s_barrier so the in-flight tile is not drained.
 __device__ uint4 ls_zero_page[2];
 
-__device__ __forceinline__ void glds16(const void* src, uint4* lds_dst) {
-  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
-}
 
 template <int KS, bool TAPU, int BK = 64>
 __device__ __forceinline__ const void* a_src(const ConvArgs& a, int kt, int c, int m, const RowGeo& g) {
@@ -626,15 +619,6 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
 }
 
-template <int N> __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
-
-// LDS image of one operand tile: rows of BK bf16, 16-B chunks XOR-swizzled so
-// the 16-lane groups of a ds_read_b128 fragment read hit distinct bank slots.
-template <int BK>
-__device__ __forceinline__ int swz_bk(int row, int c) {
-  if (BK == 64) return row * 8 + (c ^ ((row >> 1) & 7));
-  return row * 4 + (c ^ ((-(row >> 2)) & 3));
-}
 
 // Operand DMA through buffer descriptors for a BM x BN x 64 tile whose threads each
 // move AI A pieces and BI B pieces of 16 B per K-tile (LDS images lane-linear per

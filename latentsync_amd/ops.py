@@ -261,6 +261,57 @@ def attention(q, k, v, o, *, batch, z2, heads, nq, nk, head_dim, qs, ks, vs, os_
     return o
 
 
+class TemporalPack:
+    """Packed operands of ls_temporal_attention for one VersatileAttention block."""
+
+    def __init__(self, w, gamma, bpe, C, heads, eps=1e-5):
+        self.w, self.gamma, self.bpe, self.C, self.heads, self.eps = w, gamma, bpe, C, heads, eps
+
+
+def pack_temporal(wq, wk, wv, ln_weight, ln_bias, pe, heads, device):
+    """ls_temporal_attention operands (include/ls_hip.h) from the reference tensors of one
+    VersatileAttention block and its LayerNorm (motion_module.py:203-218, :262-313):
+    q|k|v rows per 80-channel group as (q_t, k_t, v_t) 16-row tiles, the q rows scaled
+    by log2(e)/sqrt(d) (the kernel's softmax works in log2 units), gamma, and
+    beta + pe[f] for f < 16."""
+    C = wq.shape[0]
+    d = C // heads
+    sc = math.log2(math.e) / math.sqrt(d)
+    rows = []
+    for g in range(C // 80):
+        for t in range(5):  # (q_t, k_t, v_t): 16-channel tiles of the group in turn
+            cs = slice(80 * g + 16 * t, 80 * g + 16 * t + 16)
+            rows += [wq[cs].float() * sc, wk[cs].float(), wv[cs].float()]
+    w = torch.cat(rows).to(torch.bfloat16)
+    bpe = ln_bias.float().reshape(1, C).repeat(16, 1)
+    if pe is not None:
+        n = min(16, pe.shape[0])
+        bpe[:n] += pe[:n].float().cpu()
+    return TemporalPack(w.to(device).contiguous(), ln_weight.float().to(device).contiguous(),
+                        bpe.to(device).contiguous(), C, heads)
+
+
+def temporal_attention_ok(C, heads, F, S):
+    """Shapes ls_temporal_attention takes (else the q|k|v GEMM + ls_attention path)."""
+    return heads == 8 and 1 <= F <= 16 and ((C == 320 and S % 16 == 0) or (C == 640 and S % 8 == 0))
+
+
+def temporal_attention(x2d, pk: TemporalPack, n_samples, F, S, out=None):
+    """LayerNorm + pe + q|k|v + temporal SDPA of a motion-module attention block in one
+    launch (ls_temporal_attention).  x2d (n_samples*F*S, C) rows "(b f) s" -> o, same rows."""
+    lib = _lib.load()
+    rows, C_ = x2d.shape
+    assert C_ == pk.C and rows == n_samples * F * S and x2d.stride(1) == 1
+    if out is None:
+        out = torch.empty((rows, C_), dtype=torch.bfloat16, device=x2d.device)
+    d = _lib.TAttnDesc()
+    d.x, d.ldx, d.gamma, d.bpe, d.w = _p(x2d), x2d.stride(0), _p(pk.gamma), _p(pk.bpe), _p(pk.w)
+    d.o, d.ldo = _p(out), out.stride(0)
+    d.C, d.heads, d.n_samples, d.F, d.S, d.eps = pk.C, pk.heads, n_samples, F, S, pk.eps
+    check(lib.ls_temporal_attention(C.byref(d), _stream()), "ls_temporal_attention")
+    return out
+
+
 def attention_fp8_workspace_bytes(*, batch, heads, nk, head_dim):
     lib = _lib.load()
     d = _lib.AttnDesc()

@@ -22,6 +22,7 @@ activations with frames folded into the image index:
       attention over frames via strided views -> out-proj) -> GEGLU FF -> proj_out
 """
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -31,6 +32,9 @@ from .config import STAGE2_MODEL
 from .packing import geglu_interleave, pack_weight, pad_bias
 from .schema import unet_param_shapes
 from .weights import fill_state_dict
+
+# LS_FUSED_TEMPORAL=0: the motion attention as q|k|v GEMM + ls_attention (A/B switch)
+_FUSED_TEMPORAL = os.environ.get("LS_FUSED_TEMPORAL", "1") != "0"
 
 _DEFAULTS = dict(
     sample_size=None, in_channels=4, out_channels=4, center_input_sample=False, flip_sin_to_cos=True, freq_shift=0,
@@ -220,9 +224,13 @@ class _Motion:
                 pe = pe.to(dv.device).contiguous()
             else:
                 pe = None
+            ln = (sd[f"{b}.norms.{i}.weight"], sd[f"{b}.norms.{i}.bias"])
+            wqkv = [sd[f"{a}.to_{n}.weight"] for n in "qkv"]
             self.attn.append(dict(
-                qkv=dv.packed_ln(torch.cat([sd[f"{a}.to_{n}.weight"] for n in "qkv"], 0), None,
-                                 (sd[f"{b}.norms.{i}.weight"], sd[f"{b}.norms.{i}.bias"]), pe=pe),
+                qkv=dv.packed_ln(torch.cat(wqkv, 0), None, ln, pe=pe),
+                # LayerNorm + pe + q|k|v + temporal SDPA in one kernel (ls_temporal_attention)
+                fused=ops.pack_temporal(*wqkv, *ln, pe, heads, dv.device) if c in (320, 640) and heads == 8
+                else None,
                 o=dv.packed(a + ".to_out.0.weight", a + ".to_out.0.bias")))
             i += 1
         self.ff1 = dv.packed_ln(sd[b + ".ff.net.0.proj.weight"], sd[b + ".ff.net.0.proj.bias"],
@@ -241,14 +249,19 @@ class _Motion:
         h = ops.conv(x, self.proj_in, aff=(sc[0], sc[1], 1, False), aff_materialize=True,
                      stats_out=lns).view(rows, C)
         o = torch.empty((rows, C), dtype=torch.bfloat16, device=x.device)
+        fuse = _FUSED_TEMPORAL and ops.temporal_attention_ok(C, self.heads, F, S)
         for a in self.attn:
-            pk = a["qkv"]  # LN (+ positional encoding, as the W pe row table) folded in
-            rv = (pk.pe_rows, S, pk.pe_rows.shape[1], F) if pk.pe_rows is not None else None
-            qkv = ops.linear(h, pk, ln_stats=lns, rowvec=rv)
-            # "(b f) s c -> (b s) f c": batch (b, s), sequence f
-            st = (F * S * 3 * C, 3 * C, S * 3 * C, d)
-            ops.attention(qkv, qkv[:, C:], qkv[:, 2 * C:], o, batch=B * S, z2=S, heads=self.heads, nq=F, nk=F,
-                          head_dim=d, qs=st, ks=st, vs=st, os_=(F * S * C, C, S * C, d))
+            if fuse and a["fused"] is not None:
+                # LayerNorm (+pe) -> q|k|v -> SDPA over the frames: q|k|v never reach HBM
+                ops.temporal_attention(h, a["fused"], B, F, S, out=o)
+            else:
+                pk = a["qkv"]  # LN (+ positional encoding, as the W pe row table) folded in
+                rv = (pk.pe_rows, S, pk.pe_rows.shape[1], F) if pk.pe_rows is not None else None
+                qkv = ops.linear(h, pk, ln_stats=lns, rowvec=rv)
+                # "(b f) s c -> (b s) f c": batch (b, s), sequence f
+                st = (F * S * 3 * C, 3 * C, S * 3 * C, d)
+                ops.attention(qkv, qkv[:, C:], qkv[:, 2 * C:], o, batch=B * S, z2=S, heads=self.heads, nq=F, nk=F,
+                              head_dim=d, qs=st, ks=st, vs=st, os_=(F * S * C, C, S * C, d))
             h = ops.linear(o, a["o"], res=h, stats_out=lns)
         g = ops.linear(h, self.ff1, act=ops.ACT_GEGLU, ln_stats=lns)
         h = ops.linear(g, self.ff2, res=h)

@@ -167,14 +167,16 @@ def test_engines_dropped_during_capture(gpu):
         dead = WindowEngine(unet, vae, DDIMScheduler(**SCHED), Fr, Rr, steps, 1.0)
         dead.load(*inp)
         dead.run()
-        dead.cycle = dead  # unreachable after `del`, freed only by the collector
+        dead.cycle = dead  # a cycle: only the collector frees it
+        holder = [dead]    # ... and not before the capture below drops this last reference
         del dead
         eng = WindowEngine(unet, vae, DDIMScheduler(**SCHED), Fr, Rr, steps, 1.0)
         real_step = eng._step
 
         def step_with_gc():
-            if torch.cuda.is_current_stream_capturing():
-                gc.collect()  # frees `dead` while the step graph is being captured
+            if torch.cuda.is_current_stream_capturing() and holder:
+                holder.clear()
+                gc.collect()  # frees the dead engine while the step graph is being captured
             real_step()
         eng._step = step_with_gc
         eng.load(*inp)
