@@ -7,8 +7,10 @@ build/ objects and links latentsync_amd/libls_hip.so.  No CUDA, no dual path.
 import concurrent.futures as cf
 import os
 import re
+import shutil
 import subprocess
 import sys
+import tempfile
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
@@ -51,6 +53,26 @@ def _spills(stderr):
     return bad
 
 
+OBJDUMP = os.environ.get("LLVM_OBJDUMP", "/opt/rocm/lib/llvm/bin/llvm-objdump")
+_PK_OPSEL = re.compile(r"v_pk_(?:fma|mul|add)_f32\b[^\n]*\bop_sel:\[([01,]+)\]")
+
+
+def _packed_opsel(obj):
+    """Disassembled gfx950 instructions of `obj` of the packed-fp32 op_sel form that
+    miscomputes beside MFMAs (see FLAGS); [] when clean or when llvm-objdump is absent."""
+    if not os.path.exists(OBJDUMP):
+        return []
+    with tempfile.TemporaryDirectory() as td:
+        cp = os.path.join(td, "k.o")
+        shutil.copy(obj, cp)
+        r = subprocess.run([OBJDUMP, "--offloading", cp], capture_output=True, text=True, cwd=td)
+        dev = [f for f in os.listdir(td) if "gfx950" in f]
+        if r.returncode != 0 or not dev:
+            raise RuntimeError(f"could not extract the gfx950 code object of {obj}: {r.stderr}")
+        r = subprocess.run([OBJDUMP, "-d", "--mcpu=gfx950", os.path.join(td, dev[0])], capture_output=True, text=True)
+    return [m.group(0).split("//")[0].strip() for m in _PK_OPSEL.finditer(r.stdout) if "1" in m.group(1)]
+
+
 def _compile(src, obj, dep_time):
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), dep_time):
         return obj, None
@@ -62,6 +84,10 @@ def _compile(src, obj, dep_time):
     if bad:
         os.remove(obj)
         return obj, "register spills in counted-vmcnt kernels:\n" + "\n".join(bad)
+    bad = _packed_opsel(obj)
+    if bad:
+        os.remove(obj)
+        return obj, f"{len(bad)} packed-fp32 op_sel instructions (wrong beside MFMAs on gfx950), e.g.:\n" + "\n".join(bad[:4])
     return obj, None
 
 

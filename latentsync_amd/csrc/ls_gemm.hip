@@ -1571,8 +1571,10 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
     }
   }
   if (AF) {
-    // x * scale[s][c] + shift[s][c] (+ SiLU), rounded to bf16 like ls_groupnorm_apply's
-    // materialised output; the block's rows lie in one sample (host: pix_per_sample % BM == 0)
+    // x * scale[s][c] + shift[s][c], rounded to bf16 like ls_groupnorm_apply's materialised
+    // output; the block's rows lie in one sample (host: pix_per_sample % BM == 0).  A SiLU
+    // after the affine goes to the register-staged kernel (rowblock_ok): beside the 80 A
+    // registers its unrolled form spills.
     const long sb = (long)((rb * BM) / a.pix_per_sample) * a.Cin + lg * 8;
     wait_vm<0>();
 #pragma unroll
@@ -1584,11 +1586,10 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
       for (int i = 0; i < FM; ++i) {
         bf16x8 v = ar[i][s];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float t = fmaf((float)v[e], sc[e], sh[e]);
-          if (a.silu_in) t = silu(t);
-          v[e] = (__bf16)t;
-        }
+        for (int e = 0; e < 8; ++e) v[e] = (__bf16)fmaf((float)v[e], sc[e], sh[e]);
+        // pin the result here: sunk past the barrier, every step's scale / shift would
+        // stay live beside the A rows and spill
+        asm volatile("" : "+v"(v));
         ar[i][s] = v;
       }
     }
@@ -1836,7 +1837,7 @@ static bool g_rb640_res = getenv("LS_GEMM_RB640_RES") != nullptr;  // A/B switch
 static bool rowblock_ok(const ls_conv_desc* d, const ConvArgs& a) {
   if (!g_rowblock || g_force_tile || g_force_regstage || d->ksize != 1 || a.C2) return false;
   // GroupNorm affine prologue: one sample per block, and not together with the LayerNorm fold
-  if (a.aff_scale && (a.ln_mr || a.pix_per_sample % (a.Cin == 320 ? 256 : 128) ||
+  if (a.aff_scale && (a.ln_mr || a.silu_in || a.pix_per_sample % (a.Cin == 320 ? 256 : 128) ||
                       ((uintptr_t)a.aff_scale | (uintptr_t)a.aff_shift) & 15))
     return false;
   // K = 640 only without a residual (the tiled kernel is faster there: 48 vs 53 us at 16x16)

@@ -14,15 +14,14 @@
 // o -- two launches and two extra full-tensor round trips per attention block.
 //
 // Layout.  A workgroup owns 2*WAVES pixels of one sample x all F (<= 16) frames; wave
-// w owns pixels s0, s0+1 as two 16-row MFMA fragments whose row (lane & 15) is the
+// w owns FM pixels as FM 16-row MFMA fragments whose row (lane & 15) is the
 // FRAME.  So a fragment is exactly one pixel's temporal sequence: the attention over
 // frames is wave-local, with no rearrange and no LDS.  The rows are gathered straight
 // from the (b f) s c activation (row (b*F + f)*S + s).
 //   * The wave's A rows (2 x 16 rows x C, bf16) live in registers; LayerNorm (+ the
 //     positional-encoding row of the lane's frame) is applied to them in place.
 //   * The packed q|k|v weights stream through an LDS ring by global_load_lds DMA, in
-//     sub-chunks of 48 (C = 320, 4 stages) or 16 (C = 640, 6 stages) output columns,
-//     NST - 1 sub-chunks ahead (one sub-chunk's MFMAs are shorter than a DMA's flight).  Columns are packed per
+//     sub-chunks of 48 (C = 320, 2 stages) or 16 (C = 640, 3 stages) output columns.  Columns are packed per
 //     80-wide group (2 heads at d = 40, 1 head at d = 80) as (q_t, k_t, v_t), t = 0..4:
 //     16-channel tiles of q, k and v in turn.
 //   * q and k tiles are computed transposed (C^T = W A^T: a lane holds 4 consecutive
@@ -37,8 +36,8 @@
 //     frame's row: the layout of the o tensor, stored 16 B per lane.
 // The q rows of W are pre-scaled by log2(e)/sqrt(d) on the host, so scores are in
 // log2 units and the softmax uses the bare v_exp_f32.
-// Config: C = 320 (d 40): 8 waves (2 per SIMD, ~210 VGPRs); C = 640 (d 80): 4 waves
-// (1 per SIMD: the A rows alone are 160 VGPRs).
+// Config (TCfg): 4-wave blocks, C = 320 (d 40) two pixels per wave, two blocks per CU;
+// C = 640 (d 80) one pixel per wave.
 #include "ls_common.h"
 
 typedef short v4i16 __attribute__((ext_vector_type(4)));
@@ -62,20 +61,27 @@ struct TAttnArgs {
 #define ABL(bit) false
 #endif
 
+// Blocks are small enough that two run on a CU at once: one
+// block's row gather, LayerNorm, softmax and o stores then overlap another block's
+// MFMAs (with one 8-wave block per CU those phases left the matrix pipe idle: ablation,
+// DESIGN.md §3).
 template <int C>
 struct TCfg {
-  static constexpr int WAVES = C == 320 ? 8 : 4;
+  static constexpr int WAVES = 4;
+  static constexpr int FM = C == 320 ? 2 : 1;       // 16-row fragments (= pixels) per wave
+  static constexpr int MINB = 2;                    // resident blocks per CU
   static constexpr int NT = WAVES * 64;
   static constexpr int KT = C / 32;                 // 32-wide k-steps of the A rows
   static constexpr int NG = C / 80;                 // 80-column groups
   static constexpr int D = C / 8;                   // head dim
   static constexpr int HG = 80 / D;                 // heads per group
   static constexpr int FN = C == 320 ? 3 : 1;       // 16-column tiles per W sub-chunk
-  static constexpr int NSC = 15 / FN;               // sub-chunks per group (tiles: q 0-4, k 5-9, v 10-14)
+  static constexpr int NSC = 15 / FN;               // sub-chunks per group (tiles q_t, k_t, v_t)
   static constexpr int BN = 16 * FN;                // W rows per sub-chunk
   static constexpr int STAGE = (C / 64) * BN * 8;   // 16-B slots per LDS stage
-  static constexpr int NST = C == 320 ? 4 : 6;      // LDS ring depth: sub-chunk c + NST - 1 lands while c computes
+  static constexpr int NST = C == 320 ? 2 : 3;      // LDS ring depth (30 / 20 KB stages, <= 80 KB per block)
   static constexpr int DPW = (STAGE / 64 + WAVES - 1) / WAVES;  // DMA wave-instructions per wave per stage
+  static constexpr int PPB = FM * WAVES;            // pixels per block
 };
 
 __device__ __forceinline__ void lds_sync() {
@@ -94,15 +100,15 @@ __device__ __forceinline__ bf16x8 kstep(uint2 lo, uint2 hi) {
 }
 
 template <int C>
-__global__ void __launch_bounds__(TCfg<C>::NT) tattn_fused_kernel(TAttnArgs a) {
+__global__ void __launch_bounds__(TCfg<C>::NT, TCfg<C>::MINB) tattn_fused_kernel(TAttnArgs a) {
   using T = TCfg<C>;
   constexpr int KT = T::KT, NT = T::NT, BN = T::BN, STAGE = T::STAGE, NSC = T::NSC, NG = T::NG;
-  constexpr int D = T::D, HG = T::HG, FN = T::FN;
+  constexpr int D = T::D, HG = T::HG, FN = T::FN, FM = T::FM;
   extern __shared__ __attribute__((aligned(16))) uint4 lds_w[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, lg = lane >> 4;
   const int b = blockIdx.x / a.blocks_per_sample, pg = blockIdx.x - b * a.blocks_per_sample;
-  const int s0 = pg * (2 * T::WAVES) + 2 * wid;  // this wave's pixels s0, s0 + 1
+  const int s0 = pg * T::PPB + FM * wid;  // this wave's pixels s0 .. s0 + FM - 1
   const int f = l16;                             // the frame of this lane's rows
   const bool live = f < a.F;
   const long row0 = ((long)b * a.F + f) * a.S + s0;
@@ -128,13 +134,13 @@ __global__ void __launch_bounds__(TCfg<C>::NT) tattn_fused_kernel(TAttnArgs a) {
   };
 
   // ---- A rows -> registers (lane: frame row, 8 consecutive channels per k-step)
-  bf16x8 ar[2][KT];
+  bf16x8 ar[FM][KT];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < FM; ++i) {
     const u16* src = a.x + (row0 + i) * a.ldx + lg * 8;
 #pragma unroll
     for (int s = 0; s < KT; ++s)
-      ar[i][s] = live ? *(const bf16x8*)(src + s * 32) : __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0));
+      ar[i][s] = live && !ABL(16) ? *(const bf16x8*)(src + s * 32) : __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0));
   }
   constexpr int NC = NG * NSC;  // sub-chunks in all
   constexpr int PD = T::NST - 1;  // prefetch distance
@@ -142,9 +148,9 @@ __global__ void __launch_bounds__(TCfg<C>::NT) tattn_fused_kernel(TAttnArgs a) {
   for (int c = 0; c < PD; ++c) issue(c);
   // ---- LayerNorm over the C channels of each row (the 4 lane groups of a frame hold
   // disjoint quarters), two-pass in fp32; then (x - mean) rstd gamma + (beta + pe[f])
-  float mean[2], rstd[2];
+  float mean[FM], rstd[FM];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < FM; ++i) {
     float t = 0.f;
 #pragma unroll
     for (int s = 0; s < KT; ++s)
@@ -170,7 +176,7 @@ __global__ void __launch_bounds__(TCfg<C>::NT) tattn_fused_kernel(TAttnArgs a) {
       load8f(gm + s * 32, g8);
       load8f(bp + s * 32, b8);
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < FM; ++i) {
         bf16x8 v = ar[i][s];
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = (__bf16)fmaf(((float)v[e] - mean[i]) * rstd[i], g8[e], b8[e]);
@@ -181,13 +187,13 @@ __global__ void __launch_bounds__(TCfg<C>::NT) tattn_fused_kernel(TAttnArgs a) {
   // The packed rows of a group come as (q_t, k_t, v_t) for t = 0..4 (16 channels each), so
   // S^T = K Q^T accumulates tile by tile (16x16x16 MFMAs straight from the q / k
   // accumulators) and only v^T has to stay in registers until the softmax.
-  f32x4 sacc[2][HG];   // S^T of (fragment, head): key 4 lg + r, query l16
-  uint2 qt[2];         // the current tile's q (C^T layout: frame row, 4 channels)
-  v4i16 vt[2][5];      // v^T tiles (channel rows, 4 frames per lane)
+  f32x4 sacc[FM][HG];  // S^T of (fragment, head): key 4 lg + r, query l16
+  uint2 qt[FM];        // the current tile's q (C^T layout: frame row, 4 channels)
+  v4i16 vt[FM][5];     // v^T tiles (channel rows, 4 frames per lane)
 
   for (int g = 0; g < NG; ++g) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int hh = 0; hh < HG; ++hh) sacc[i][hh] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -202,9 +208,9 @@ __global__ void __launch_bounds__(TCfg<C>::NT) tattn_fused_kernel(TAttnArgs a) {
       lds_sync();  // ... everyone's; the stage of sub-chunk c - 1 is free again
       if (c + PD < NC && !ABL(4)) issue(c + PD);
       const uint4* cur = lds_w + (c % T::NST) * STAGE;
-      f32x4 acc[2][FN];
+      f32x4 acc[FM][FN];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
       // fragments of k-step s + 1 are read while the MFMAs of k-step s issue (double
@@ -222,7 +228,7 @@ __global__ void __launch_bounds__(TCfg<C>::NT) tattn_fused_kernel(TAttnArgs a) {
           for (int j = 0; j < FN; ++j) bw[(s + 1) & 1][j] = frag(s + 1, j);
         }
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int j = 0; j < FN; ++j) {
             if ((sc * FN + j) % 3 == 2)  // v: C = A W^T
@@ -235,7 +241,7 @@ __global__ void __launch_bounds__(TCfg<C>::NT) tattn_fused_kernel(TAttnArgs a) {
       for (int j = 0; j < FN; ++j) {
         const int idx = sc * FN + j, kind = idx % 3, t = idx / 3;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < FM; ++i) {
           const uint2 pk = pack4(acc[i][j], 1.f);
           if (kind == 0) {
             qt[i] = pk;
@@ -258,7 +264,7 @@ __global__ void __launch_bounds__(TCfg<C>::NT) tattn_fused_kernel(TAttnArgs a) {
       if (sc == NSC - 1 && !ABL(1)) {
         // ---- softmax + P V of this group's heads, per fragment (pixel)
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < FM; ++i) {
           uint2 ot[6];
           ot[5] = make_uint2(0, 0);
 #pragma unroll
@@ -302,7 +308,7 @@ __global__ void __launch_bounds__(TCfg<C>::NT) tattn_fused_kernel(TAttnArgs a) {
             const auto rx = __builtin_amdgcn_permlane16_swap(ot[2 * p].x, ot[2 * p + 1].x, false, false);
             const auto ry = __builtin_amdgcn_permlane16_swap(ot[2 * p].y, ot[2 * p + 1].y, false, false);
             const int d = 32 * p + 16 * (lg & 1) + 4 * (lg & 2);
-            if (live && d < 80) *(uint4*)(orow + d) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+            if (live && d < 80 && !ABL(8)) *(uint4*)(orow + d) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
           }
         }
       }
@@ -332,7 +338,7 @@ extern "C" int ls_temporal_attention(const ls_tattn_desc* d, void* stream) {
   if (d->C != 320 && d->C != 640) return fail(LS_ERR_INVALID, "ls_temporal_attention: C must be 320 or 640");
   if (d->heads != 8) return fail(LS_ERR_INVALID, "ls_temporal_attention: 8 heads");
   if (d->F < 1 || d->F > 16) return fail(LS_ERR_INVALID, "ls_temporal_attention: 1 <= F <= 16 frames");
-  const int ppb = d->C == 320 ? 2 * TCfg<320>::WAVES : 2 * TCfg<640>::WAVES;  // pixels per block
+  const int ppb = d->C == 320 ? TCfg<320>::PPB : TCfg<640>::PPB;  // pixels per block
   if (d->S <= 0 || d->S % ppb || d->n_samples <= 0)
     return fail(LS_ERR_INVALID, "ls_temporal_attention: S must be a positive multiple of the block's pixels");
   if (d->ldx % 8 || d->ldo % 8 || d->ldx < d->C || d->ldo < d->C)
