@@ -178,12 +178,26 @@ def step_probe(engine, device):
                 blocks[-1][1] = ev()
         return call
 
-    ops.conv, ops.attention = conv, attention
+    orig_tattn = ops.temporal_attention
+
+    def temporal_attention(x2d, pk, n_samples, F, S, out=None):
+        # fused LayerNorm + q|k|v GEMM + seq-F SDPA (ls_temporal_attention): the GEMM's
+        # 2*rows*3C*C and the SDPA's 4*(n_samples*S)*heads*F*F*d FLOPs (block totals only:
+        # the "attention" SDPA figure stays the ls_attention launches)
+        r = orig_tattn(x2d, pk, n_samples, F, S, out=out)
+        rows, C = x2d.shape
+        fg = 2.0 * rows * 3 * C * C
+        fa = 4.0 * n_samples * S * pk.heads * F * F * (C // pk.heads)
+        if depth[0]:
+            blocks[-1][2] += fg + fa
+        return r
+
+    ops.conv, ops.attention, ops.temporal_attention = conv, attention, temporal_attention
     U._Transformer.__call__, U._Motion.__call__ = wrap(orig_t), wrap(orig_m)
     try:
         engine._step()
     finally:
-        ops.conv, ops.attention = orig_conv, orig_attn
+        ops.conv, ops.attention, ops.temporal_attention = orig_conv, orig_attn, orig_tattn
         U._Transformer.__call__, U._Motion.__call__ = orig_t, orig_m
     torch.cuda.synchronize(device)
 

@@ -37,7 +37,8 @@ def _deps():
 # Kernels that pace their operand DMA with counted `s_waitcnt vmcnt(N)`: a register
 # (VGPR) spill adds scratch loads/stores to the vmcnt queue and silently breaks the count,
 # so the build refuses any spill in them (hipcc resource-usage remarks).
-COUNTED_VMCNT = ("gemm_rowblock_kernel", "conv_gemm_dma_kernel", "attn5_kernel", "attn8_kernel", "tattn_fused_kernel")
+COUNTED_VMCNT = ("gemm_rowblock_kernel", "conv_gemm_dma_kernel", "attn5_kernel", "attn8_kernel", "tattn_fused_kernel",
+                 "attnw_kernel")
 
 
 def _spills(stderr):

@@ -730,6 +730,262 @@ static int launch_attn5(const AttnArgs& a, int batch, int heads, hipStream_t s) 
   return check_launch("attn5_kernel");
 }
 
+// attnw: wide heads -- the SD-VAE mid-block attention (1 head, d = 512, N = h w tokens;
+// diffusers Attention).  Replaces attn_kernel<512,4> (0.068 of the
+// dense peak: K / V staged synchronously behind two barriers per tile, no prefetch, one
+// 4-wave block per CU).  A wave owns QG 16-query fragments at the full head dim (Q and
+// the O^T accumulator in registers: 64 + 128 VGPRs at QG = 1, so two waves per SIMD and
+// eight per block share each K / V tile; QG = 2 would halve the LDS fragment reads per
+// MFMA but needs 384 registers, and the compiler spills it even at one wave per SIMD).
+//   * 32-key tiles by buffer_load ... lds DMA, "chunk-plane" layout (plane c = dims
+//     8c .. 8c + 7 of the tile's 32 keys; one wave-instruction moves two planes), K planes
+//     plain (ds_read_b128 fragments conflict-free), V planes with the key rotated by 8 per
+//     plane (the ds_read_b64_tr_b16 V^T reads conflict-free, as attn5); two 64-KB stages,
+//     the next tile's DMA issued under the current tile's MFMAs.
+//   * fragment reads software-pipelined PF k-steps ahead from one lane base plus
+//     immediate offsets (per-fragment addresses hoisted out of the tile loop each held a
+//     register and spilled the kernel);
+//   * S^T = K Q^T with the running max subtracted by the MFMA (C = -m), lazy rescale
+//     (threshold 10, one ballot per tile), bf16 P straight into O^T += V^T P^T (attn5's
+//     arithmetic).
+template <int D, int QG, int NW, int PF = 1, bool SB = true>
+__global__ void __launch_bounds__(NW * 64, 1) attnw_kernel(AttnArgs a, int nqb, int heads) {
+  constexpr int KT = 32;                  // keys per tile
+  constexpr int NPL = D / 8;              // 16-B planes per operand row
+  constexpr int PLANE = KT * 8;           // u16 per plane
+  constexpr int STAGE = 2 * NPL * PLANE;  // K planes, then V planes
+  constexpr int KC = D / 32;              // QK^T k-steps
+  constexpr int ND = D / 16;              // O^T fragments per query group
+  constexpr int QPB = NW * 16 * QG;       // queries per block
+  constexpr int NDMA = NPL / NW;          // DMA wave-instructions per wave per tile (2 planes each)
+  constexpr float TAU = 10.f;
+  static_assert(D % 64 == 0 && NPL % NW == 0, "attnw: d multiple of 64");
+  extern __shared__ __attribute__((aligned(16))) u16 sm[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lb = attn_xcd_remap(blockIdx.x, gridDim.x);
+  const int qblk = lb % nqb, pair = lb / nqb;
+  const int h = pair % heads;
+  const int b = pair / heads;
+  const long b1 = b / a.z2, b2 = b - b1 * a.z2;
+  const u16* qb = a.q + b1 * a.q_sb1 + b2 * a.q_sb2 + (long)h * a.q_sh;
+  const u16* kb = a.k + b1 * a.k_sb1 + b2 * a.k_sb2 + (long)h * a.k_sh;
+  const u16* vb = a.v + b1 * a.v_sb1 + b2 * a.v_sb2 + (long)h * a.v_sh;
+  u16* ob = a.o + b1 * a.o_sb1 + b2 * a.o_sb2 + (long)h * a.o_sh;
+  const int q0 = qblk * QPB + wid * 16 * QG;
+  const int lq = lane & 15, lg = lane >> 4;
+
+  const float c2 = a.scale_log2;
+  bf16x8 qf[QG][KC];
+#pragma unroll
+  for (int g = 0; g < QG; ++g)
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      const int q = q0 + g * 16 + lq;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (q < a.nq) v = *(const uint4*)(qb + (long)q * a.q_si + kc * 32 + lg * 8);
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] *= c2;
+      qf[g][kc] = __builtin_bit_cast(bf16x8, pack8(f));
+    }
+
+  // DMA of tile t: wave w issues instructions j = w + NW i; j < NPL / 2 moves K planes
+  // 2j, 2j + 1 (lane: plane 2j + lane / 32, key lane % 32), the rest V planes with the
+  // key rotated by 8 per plane (position (key + 8 c) % 32)
+  const uint32_t kst = (uint32_t)a.k_si * 2, vst = (uint32_t)a.v_si * 2;
+  const i32x4 krs = buffer_rsrc(kb, (uint32_t)(a.nk - 1) * kst + D * 2);
+  const i32x4 vrs = buffer_rsrc(vb, (uint32_t)(a.nk - 1) * vst + D * 2);
+  auto issue = [&](int t) {
+    u16* st = sm + (t & 1) * STAGE;
+#pragma unroll
+    for (int i = 0; i < NDMA; ++i) {
+      const int j = wid + NW * i;  // wave-uniform
+      const bool isv = j >= NPL / 2;
+      const int jj = isv ? j - NPL / 2 : j;
+      const int c = 2 * jj + (lane >> 5);
+      const int key = isv ? (((lane & 31) - 8 * c) & 31) : (lane & 31);
+      ls_raw_buffer_load_lds(isv ? vrs : krs,
+                             (__attribute__((address_space(3))) void*)(st + (isv ? NPL : 0) * PLANE + 2 * jj * PLANE), 16,
+                             key * (int)(isv ? vst : kst) + c * 16, t * KT * (int)(isv ? vst : kst), 0, 0);
+    }
+  };
+
+  f32x4 oacc[QG][ND];
+#pragma unroll
+  for (int g = 0; g < QG; ++g)
+#pragma unroll
+    for (int i = 0; i < ND; ++i) oacc[g][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m[QG], l[QG];
+  f32x4 negm[QG];
+#pragma unroll
+  for (int g = 0; g < QG; ++g) {
+    m[g] = 0.f;
+    l[g] = 0.f;
+    negm[g] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+
+  const int ntile = (a.nk + KT - 1) / KT;
+  issue(0);
+  for (int t = 0; t < ntile; ++t) {
+    attn_wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // tile t landed everywhere; every wave is past tile t - 1
+    asm volatile("" ::: "memory");
+    if (t + 1 < ntile) issue(t + 1);
+    const u16* Ks = sm + (t & 1) * STAGE;
+    const u16* Vs = Ks + NPL * PLANE;
+    // (software-pipelined PF k-steps ahead; SB fences each step with sched_barrier)
+    f32x4 s[QG][2];
+    // (one lane base + immediate offsets: per-fragment addresses hoisted out of the tile
+    // loop would each hold a register)
+    const u16* kl = Ks + lg * PLANE + lq * 8;
+    auto kread = [&](int kc, int f) {
+      return __builtin_bit_cast(bf16x8, *(const uint4*)(kl + kc * 4 * PLANE + f * 128));
+    };
+    bf16x8 kq[PF][2];  // fragments of k-steps kc .. kc + PF - 1 in flight
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+      kq[p][0] = kread(p, 0);
+      kq[p][1] = kread(p, 1);
+    }
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      const bf16x8 k0 = kq[kc % PF][0], k1 = kq[kc % PF][1];
+      if (kc + PF < KC) {
+        kq[kc % PF][0] = kread(kc + PF, 0);
+        kq[kc % PF][1] = kread(kc + PF, 1);
+      }
+#pragma unroll
+      for (int g = 0; g < QG; ++g) {
+        s[g][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf[g][kc], kc == 0 ? negm[g] : s[g][0], 0, 0, 0);
+        s[g][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf[g][kc], kc == 0 ? negm[g] : s[g][1], 0, 0, 0);
+      }
+      if (SB) __builtin_amdgcn_sched_barrier(0);
+    }
+    const int t0 = t * KT;
+    float mt[QG];
+    bool need_any = t == 0;
+#pragma unroll
+    for (int g = 0; g < QG; ++g) {
+      if (t0 + KT > a.nk) {
+#pragma unroll
+        for (int f = 0; f < 2; ++f)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (t0 + 16 * f + 4 * lg + r >= a.nk) s[g][f][r] = -INFINITY;
+      }
+      float x = __builtin_elementwise_maximum(__builtin_elementwise_maximum(s[g][0][0], s[g][0][1]),
+                                              __builtin_elementwise_maximum(s[g][0][2], s[g][0][3]));
+      x = __builtin_elementwise_maximum(
+          x, __builtin_elementwise_maximum(__builtin_elementwise_maximum(s[g][1][0], s[g][1][1]),
+                                           __builtin_elementwise_maximum(s[g][1][2], s[g][1][3])));
+      mt[g] = xor16_32_max(x);
+      need_any |= mt[g] > TAU;
+    }
+    if (__builtin_amdgcn_ballot_w64(need_any)) {
+#pragma unroll
+      for (int g = 0; g < QG; ++g) {
+        const bool need = t == 0 || mt[g] > TAU;
+        const float dlt = need ? mt[g] : 0.f;
+        const float alpha = t == 0 ? 0.f : fast_exp2(-dlt);
+        m[g] += dlt;
+        negm[g] = (f32x4){-m[g], -m[g], -m[g], -m[g]};
+#pragma unroll
+        for (int f = 0; f < 2; ++f) s[g][f] -= dlt;
+#pragma unroll
+        for (int i = 0; i < ND; ++i) oacc[g][i] *= alpha;
+        l[g] *= alpha;
+      }
+    }
+    bf16x8 pb[QG];
+#pragma unroll
+    for (int g = 0; g < QG; ++g) {
+      float ps = 0.f;
+#pragma unroll
+      for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = fast_exp2(s[g][f][r]);
+          ps += p;
+          pb[g][4 * f + r] = (__bf16)p;
+        }
+      l[g] += ps;
+    }
+    // O^T += V^T P^T: a lane reads 4 dims of key 4 lg + qq (and + 16) from plane
+    // 2 nd + pp / 2 at its rotated position
+    // plane pl = 2 nd + pp / 2 holds key k at position (k + 8 pl) % 32: for even nd the
+    // low read (key) sits at rotation re, the high one (key + 16) at ro; odd nd swaps them
+    const int qq = lq >> 2, pp = lq & 3;
+    const int key = 4 * lg + qq;
+    const u16* vl = Vs + (pp >> 1) * PLANE + (pp & 1) * 4;
+    const u16* pe = vl + ((key + 8 * (pp >> 1)) & 31) * 8;
+    const u16* po = vl + ((key + 16 + 8 * (pp >> 1)) & 31) * 8;
+    auto vread = [&](int nd) {
+      const u16* lop = ((nd & 1) ? po : pe) + 2 * nd * PLANE;
+      const u16* hip = ((nd & 1) ? pe : po) + 2 * nd * PLANE;
+      const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)lop);
+      const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)hip);
+      const short __attribute__((ext_vector_type(8))) av = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      return __builtin_bit_cast(bf16x8, av);
+    };
+    bf16x8 vq[PF];
+#pragma unroll
+    for (int p = 0; p < PF; ++p) vq[p] = vread(p);
+#pragma unroll
+    for (int nd = 0; nd < ND; ++nd) {
+      const bf16x8 vf = vq[nd % PF];
+      if (nd + PF < ND) vq[nd % PF] = vread(nd + PF);
+#pragma unroll
+      for (int g = 0; g < QG; ++g) oacc[g][nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[g], oacc[g][nd], 0, 0, 0);
+      if (SB) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < QG; ++g) {
+    const float inv = 1.f / xor16_32_sum(l[g]);
+    const int q = q0 + g * 16 + lq;
+    if (q < a.nq) {
+      u16* orow = ob + (long)q * a.o_si;
+#pragma unroll
+      for (int nd = 0; nd < ND; ++nd)
+        *(uint2*)(orow + nd * 16 + 4 * lg) = make_uint2(pack2(oacc[g][nd][0] * inv, oacc[g][nd][1] * inv),
+                                                        pack2(oacc[g][nd][2] * inv, oacc[g][nd][3] * inv));
+    }
+  }
+}
+
+template <int D, int QG, int NW, int PF, bool SB>
+static int launch_attnw(const AttnArgs& a, int batch, int heads, hipStream_t s) {
+  const int nqb = cdiv(a.nq, NW * 16 * QG);
+  const long nblk = (long)nqb * heads * batch;
+  if (nblk > 0x7fffffff) return fail(LS_ERR_INVALID, "ls_attention: grid too large");
+  const size_t shm = (size_t)2 * 2 * (D / 8) * 32 * 8 * sizeof(u16);  // two stages of K + V tiles
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)attnw_kernel<D, QG, NW, PF, SB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)shm);
+    attr_set = true;
+  }
+  attnw_kernel<D, QG, NW, PF, SB><<<(int)nblk, NW * 64, shm, s>>>(a, nqb, heads);
+  return check_launch("attnw_kernel");
+}
+
+static const int g_attnw_variant = getenv("LS_ATTNW_VARIANT") ? atoi(getenv("LS_ATTNW_VARIANT")) : 0;  // A/B switch
+
+static int launch_attnw512(const AttnArgs& a, int batch, int heads, hipStream_t s) {
+  // same-box A/B (scripts/attn_bench.py VAE=1, 512 images at 32^2 / 64 at 64^2):
+  // PF 1 fenced 1673 / 2934 us, PF 1 unfenced 1609 / 2818, PF 2 fenced 1598 / 2793,
+  // PF 2 unfenced 1609 / 2812 (attn_kernel<512,4> before: 6449 / 11858)
+  switch (g_attnw_variant) {
+    case 1: return launch_attnw<512, 1, 8, 1, false>(a, batch, heads, s);
+    case 2: return launch_attnw<512, 1, 8, 1, true>(a, batch, heads, s);
+    case 3: return launch_attnw<512, 1, 8, 2, false>(a, batch, heads, s);
+    default: return launch_attnw<512, 1, 8, 2, true>(a, batch, heads, s);
+  }
+}
+
 template <int KC, int ND, int DSUM, bool ONE>
 static int launch_attn3_(const AttnArgs& a, int batch, int heads, hipStream_t s) {
   const dim3 grid(cdiv(a.nq, 128), heads, batch);
@@ -1414,6 +1670,7 @@ using namespace ls;
 
 static bool g_attn_v1 = getenv("LS_ATTN_V1") != nullptr;  // A/B switch: force the 16-query kernel
 static bool g_attn_v3 = getenv("LS_ATTN_V3") != nullptr;  // A/B switch: attn3 for d = 40 too
+static bool g_attnw_off = getenv("LS_ATTNW_OFF") != nullptr;  // A/B switch: d = 512 on attn_kernel
 static bool g_seq_valu = getenv("LS_ATTN_SEQ_VALU") != nullptr;  // A/B switch: dot-product short-sequence kernel
 static bool g_seq160_valu = getenv("LS_ATTN_SEQ160_VALU") != nullptr;  // A/B switch: ... for d = 160 only
 
@@ -1525,6 +1782,14 @@ extern "C" int ls_attention(const ls_attn_desc* d, void* stream) {
       default: return launch_attn3<5, 10, 0>(a, d->batch, d->heads, s);
     }
   }
+  // d = 512 (the VAE mid attention): the head dim split over wave pairs (attnw)
+  if (D == 512 && !g_attn_v1 && !g_attnw_off && d->q_si % 8 == 0 && d->k_si % 8 == 0 && d->v_si % 8 == 0 &&
+      d->o_si % 4 == 0 && (((uintptr_t)d->q | (uintptr_t)d->k | (uintptr_t)d->v) & 15) == 0 &&
+      ((uintptr_t)d->o & 7) == 0 && (d->q_sb1 | d->q_sb2 | d->q_sh | d->k_sb1 | d->k_sb2 | d->k_sh | d->v_sb1 |
+                                      d->v_sb2 | d->v_sh) % 8 == 0 &&
+      (d->o_sb1 | d->o_sb2 | d->o_sh) % 4 == 0 &&
+      ((long)(d->nk + 32) * std::max(d->k_si, d->v_si) + D) * 2 < (1L << 31))
+    return launch_attnw512(a, d->batch, d->heads, s);
 #define LS_ATTN(DPV)                                                              \
   return small ? launch_attn<DPV, 2>(a, d->batch, d->heads, s)                    \
                : launch_attn<DPV, 4>(a, d->batch, d->heads, s);

@@ -18,6 +18,9 @@ if os.environ.get("CFG4"):  # configs[4]: 64^2 latent (WINDOWS windows of 16 fra
     CASES = [("c4 spatial L0 d40", 16 * W, 4096, 4096, 8, 40, "self"),
              ("c4 spatial L1 d80", 16 * W, 1024, 1024, 8, 80, "self"),
              ("c4 spatial L2 d160", 16 * W, 256, 256, 8, 160, "self")]
+if os.environ.get("VAE"):  # SD-VAE mid attention: 1 head, d = 512, 32x32 (256^2) / 64x64 (512^2) latents
+    CASES = [("vae mid 32^2 d512", 32 * W, 1024, 1024, 1, 512, "self"),
+             ("vae mid 64^2 d512", 4 * W, 4096, 4096, 1, 512, "self")]
 FP8 = bool(os.environ.get("ATTN_FP8"))  # self attention through ls_attention_fp8
 
 

@@ -157,7 +157,9 @@ def _sdpa(q, k, v, scale=None):
                                             # configs[4] (latent 64^2): spatial N = 4096 / 1024, audio cross
                                             (1, 4096, 4096, 8, 40), (2, 1024, 1024, 8, 80), (1, 4096, 50, 8, 40),
                                             # SD-VAE mid attention at 256^2: 1 head, d = 512, N = 1024
-                                            (2, 1024, 1024, 1, 512)])
+                                            (2, 1024, 1024, 1, 512),
+                                            # d = 512 (attnw): ragged queries / keys, two heads
+                                            (2, 300, 130, 2, 512)])
 def test_attention_spatial(gpu, n, N, Nk, heads, d):
     C = heads * d
     q = bf(rnd(n, N, C, seed=50))
@@ -169,6 +171,23 @@ def test_attention_spatial(gpu, n, N, Nk, heads, d):
     o = torch.empty_like(qd)
     ops.attention(qd, kd, vd, o, batch=n, z2=1, heads=heads, nq=N, nk=Nk, head_dim=d, qs=(N * C, 0, C, d),
                   ks=(Nk * C, 0, C, d), vs=(Nk * C, 0, C, d), os_=(N * C, 0, C, d))
+    assert rel_err(o.float().cpu(), ref) < 1.5e-2
+
+
+@pytest.mark.parametrize("qscale", [1.0, 3.0])
+def test_attention_d512_rescale(gpu, qscale):
+    """attnw (d = 512): keys whose scores grow along the sequence, so the running max moves
+    past the lazy-rescale threshold on later tiles (qscale 3: log2-unit logits past 20)."""
+    n, N, Nk, d = 2, 256, 1024, 512
+    q = rnd(n, N, d, seed=60) * qscale
+    k = rnd(n, Nk, d, seed=61) * torch.linspace(0.2, 2.0, Nk).reshape(1, Nk, 1)
+    v = rnd(n, Nk, d, seed=62)
+    q, k, v = bf(q), bf(k), bf(v)
+    ref = _sdpa(q[:, None], k[:, None], v[:, None])[:, 0]
+    qd, kd, vd = (t.to(torch.bfloat16).to(DEV) for t in (q, k, v))
+    o = torch.empty_like(qd)
+    ops.attention(qd, kd, vd, o, batch=n, z2=1, heads=1, nq=N, nk=Nk, head_dim=d, qs=(N * d, 0, d, d),
+                  ks=(Nk * d, 0, d, d), vs=(Nk * d, 0, d, d), os_=(N * d, 0, d, d))
     assert rel_err(o.float().cpu(), ref) < 1.5e-2
 
 
