@@ -234,6 +234,56 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const u16* __restrict__ x
   }
 }
 
+// The same apply with U independent 16-B loads in flight per thread.  gn_apply_kernel's
+// grid-stride walk had one load outstanding per thread (~32 KB per CU: latency-bound at
+// ~4 TB/s), and its stride (gridDim * ppb pixels) crossed a sample boundary on almost
+// every step, so the "rare" scale / shift reload ran every iteration.  Here a block owns
+// U * ppb consecutive pixels (thread: pixels base + k ppb + pl, k < U, coalesced rows),
+// issues all U loads first, and looks the sample up once per thread (a block spans at
+// most a few samples: the host keeps U * ppb <= pps).
+template <int U>
+__global__ void __launch_bounds__(256) gn_apply_u_kernel(const u16* __restrict__ x1, const u16* __restrict__ x2, int C1,
+                                                         int C2, long n_pix, long pps, const float* __restrict__ scale,
+                                                         const float* __restrict__ shift, int silu_on,
+                                                         u16* __restrict__ y, int ppb, int ccb) {
+  const int C = C1 + C2, CC = C / 8;
+  const int pl = threadIdx.x / ccb, cc = blockIdx.y * ccb + threadIdx.x - pl * ccb;
+  if (pl >= ppb || cc >= CC) return;
+  const int c = cc * 8;
+  const u16* src = c < C1 ? x1 + c : x2 + (c - C1);
+  const int lds = c < C1 ? C1 : C2;
+  const long p0 = (long)blockIdx.x * ppb * U + pl;
+  uint4 v[U];
+#pragma unroll
+  for (int k = 0; k < U; ++k) {
+    const long pix = p0 + (long)k * ppb;
+    v[k] = pix < n_pix ? *(const uint4*)(src + pix * lds) : make_uint4(0, 0, 0, 0);
+  }
+  long s_cur = p0 / pps, s_end = (s_cur + 1) * pps;
+  float sc[8], sh[8];
+  load8f(scale + s_cur * C + c, sc);
+  load8f(shift + s_cur * C + c, sh);
+#pragma unroll
+  for (int k = 0; k < U; ++k) {
+    const long pix = p0 + (long)k * ppb;
+    if (pix >= n_pix) break;
+    if (pix >= s_end) {  // (a block's range crossed into the next sample)
+      s_cur = pix / pps;
+      s_end = (s_cur + 1) * pps;
+      load8f(scale + s_cur * C + c, sc);
+      load8f(shift + s_cur * C + c, sh);
+    }
+    float f[8];
+    unpack8(v[k], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float t = fmaf(f[j], sc[j], sh[j]);
+      f[j] = silu_on ? silu(t) : t;
+    }
+    *(uint4*)(y + pix * C + c) = pack8(f);
+  }
+}
+
 // LayerNorm: 16 lanes per row (4 rows per wave, 16 per block), row cached in
 // registers, two-pass mean / variance, 16-lane shuffle reductions.
 template <int NCH>
@@ -352,6 +402,17 @@ extern "C" int ls_groupnorm_apply(const uint16_t* x1, const uint16_t* x2, int32_
   const int ccb = std::min(CC, 256);
   const int ppb = std::max(1, 256 / ccb);
   const int threads = (ppb * ccb + 63) / 64 * 64;  // 1280 channels: 3 waves, 160 live lanes
+  static const bool v1 = getenv("LS_GN_APPLY_V1") != nullptr;  // A/B switch: the grid-stride kernel
+  constexpr int U = 4;
+  const long ublocks = (n_pix + (long)U * ppb - 1) / ((long)U * ppb);
+  // (C >= 1280 -- one pixel per block pass -- stays on the grid-stride kernel: 37 vs 41 us
+  // at 8x8 / 32 windows; C <= 640 and the VAE 12-17 % faster, profiles/r03c_gn_apply_ab.txt)
+  if (!v1 && ppb >= 2 && (((uintptr_t)scale | (uintptr_t)shift) & 15) == 0 && (long)U * ppb <= pps &&
+      ublocks < 0x7fffffffL) {
+    gn_apply_u_kernel<U><<<dim3((unsigned)ublocks, cdiv(CC, ccb)), threads, 0, (hipStream_t)stream>>>(
+        x1, x2, C1, C2, n_pix, pps, scale, shift, silu_on, y, ppb, ccb);
+    return check_launch("gn_apply_u_kernel");
+  }
   const long blocks = std::min<long>(cdiv(n_pix, ppb), 16384);
   gn_apply_kernel<<<dim3((unsigned)blocks, cdiv(CC, ccb)), threads, 0, (hipStream_t)stream>>>(
       x1, x2, C1, C2, n_pix, pps, scale, shift, silu_on, y, ppb, ccb);

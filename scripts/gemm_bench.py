@@ -17,6 +17,7 @@ SHAPES = [  # (name, n_img, H, Cin, Cout, ksize, act)
     ("geglu2 1280->10240", 16, 8, 1280, 10240, 1, 1), ("ff2_2 5120->1280", 16, 8, 5120, 1280, 1, 0),
     ("qkv2 1280->3840", 16, 8, 1280, 3840, 1, 0), ("plain0 320->2560", 16, 32, 320, 2560, 1, 0), ("vae conv 128 256^2", 16, 256, 128, 128, 3, 0),
     ("vae conv 512 32^2", 16, 32, 512, 512, 3, 0),
+    ("out1 640->640", 16, 16, 640, 640, 1, 0), ("out2 1280->1280", 16, 8, 1280, 1280, 1, 0),
 ]
 
 

@@ -1,4 +1,5 @@
-"""GroupNorm stats / apply micro-benchmark on the UNet's shapes (8 windows)."""
+"""GroupNorm stats / apply micro-benchmark on the UNet's shapes (WINDOWS windows, default 32) and two
+VAE shapes (64 images).  LS_GN_APPLY_V1=1: the grid-stride apply kernel."""
 import os, statistics, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -15,7 +16,8 @@ def timeit(f, reps=20):
     return statistics.median(ts) * 1e3
 
 
-for (n, H, C) in [(128, 32, 320), (128, 16, 640), (128, 8, 1280), (128, 4, 1280), (16, 256, 128)]:
+W = int(os.environ.get('WINDOWS', '32'))
+for (n, H, C) in [(16 * W, 32, 320), (16 * W, 16, 640), (16 * W, 8, 1280), (16 * W, 4, 1280), (64, 256, 128), (64, 128, 256)]:
     x = torch.randn(n, H, H, C, device="cuda").to(torch.bfloat16)
     g, b = torch.ones(C, device="cuda"), torch.zeros(C, device="cuda")
     B = n // 16
@@ -23,5 +25,5 @@ for (n, H, C) in [(128, 32, 320), (128, 16, 640), (128, 8, 1280), (128, 4, 1280)
     sc, sh = ops.group_norm(x, 32, 1e-5, g, b, B)
     ta = timeit(lambda: ops.group_norm_apply(x, sc, sh, B, True))
     mb = x.numel() * 2 / 1e6
-    print(f"rpt={os.environ.get('LS_GN_RPT', '8'):3s} GN {n}x{H}x{H}x{C}: stats {t:7.1f} us ({mb / t:5.2f} TB/s)  "
+    print(f"v1={os.environ.get('LS_GN_APPLY_V1', '0')} GN {n}x{H}x{H}x{C}: stats {t:7.1f} us ({mb / t:5.2f} TB/s)  "
           f"apply {ta:7.1f} us ({2 * mb / ta:5.2f} TB/s)")

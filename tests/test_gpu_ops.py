@@ -509,6 +509,28 @@ def test_groupnorm_colsum_large_mean(gpu, offset):
     assert rel_err(sc.cpu(), sc2.cpu()) < 1e-3 and rel_err(sh.cpu(), sh2.cpu()) < 1e-3
 
 
+@pytest.mark.parametrize("n,S,H,C1,C2,silu", [(32, 16, 8, 320, 0, True), (24, 8, 4, 1280, 0, True),
+                                               (16, 16, 16, 640, 640, True), (6, 1, 32, 128, 0, False),
+                                               (16, 4, 2, 2560, 0, True), (5, 1, 3, 64, 32, False)])
+def test_groupnorm_apply(gpu, n, S, H, C1, C2, silu):
+    """ls_groupnorm_apply: y = act(x * scale[sample, c] + shift[sample, c]) over a channel
+    concat, samples of S images (block ranges crossing sample boundaries, ragged tails,
+    channel counts split over blockIdx.y), against the same arithmetic in fp32."""
+    C = C1 + C2
+    x1 = bf(rnd(n, H, H, C1, seed=70))
+    x2 = bf(rnd(n, H, H, C2, seed=71)) if C2 else None
+    ns = n // S
+    sc = rnd(ns, C, seed=72, scale=0.5) + 1.0
+    sh = rnd(ns, C, seed=73, scale=0.5)
+    y = ops.group_norm_apply(x1.to(torch.bfloat16).to(DEV), sc.to(DEV), sh.to(DEV), ns, silu,
+                             x2=x2.to(torch.bfloat16).to(DEV) if C2 else None).float().cpu()
+    xx = torch.cat([x1, x2], -1) if C2 else x1
+    ref = xx.reshape(ns, S, H, H, C) * sc.reshape(ns, 1, 1, 1, C) + sh.reshape(ns, 1, 1, 1, C)
+    ref = (F.silu(ref) if silu else ref).reshape(n, H, H, C)
+    err = (y - ref).abs() / (ref.abs() + 1e-2)
+    assert float(err.max()) < 1e-2
+
+
 @pytest.mark.parametrize("K,M,N,H,silu", [(320, 65536, 320, 32, False), (640, 32768, 640, 16, False),
                                           (320, 65536, 960, 32, True), (1280, 512, 1280, 16, False)])
 def test_gn_affine_fold(gpu, K, M, N, H, silu):
