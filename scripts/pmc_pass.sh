@@ -12,3 +12,4 @@ for c in FETCH_SIZE WRITE_SIZE; do
   rc=$?; echo "pmc $c rc=$rc"; [ $rc -ne 0 ] && { tail -5 gpurun_out/${tag}_$c.log; exit $rc; }
 done
 python3 scripts/pmc_traffic.py gpurun_out/${tag}_FETCH_SIZE gpurun_out/${tag}_WRITE_SIZE gpurun_out/${tag}_traffic.json
+python3 scripts/pmc_per_kernel.py gpurun_out/${tag}_FETCH_SIZE gpurun_out/${tag}_WRITE_SIZE 60 > gpurun_out/${tag}_per_kernel.txt
