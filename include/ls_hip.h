@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LS_ABI_VERSION 9
+#define LS_ABI_VERSION 10
 
 typedef enum {
   LS_OK = 0,
@@ -48,7 +48,8 @@ enum { LS_ACT_NONE = 0, LS_ACT_GEGLU = 1, LS_ACT_GELU = 2, LS_ACT_SILU = 3 };
  *   Y[m, n] = epilogue( sum_k A[m, k] * Wp[n, k] )
  *
  * A is never materialised: row m is an output pixel (img, yo, xo); column
- * k = tap*Cin + ci reads input channel ci of the tap's source pixel, from x1
+ * k reads input channel ci of the tap's source pixel -- k = tap*Cin + ci, or for
+ * ksize 3 with Cin % 64 == 0 (ABI 10) k = (ci/64)*576 + tap*64 + ci%64 -- from x1
  * (ci < C1) or x2 (ci >= C1, the fused torch.cat of the up blocks,
  * unet_blocks.py:624,745).  Optional prologue per element (fused GroupNorm
  * apply + SiLU of ResnetBlock3D, resnet.py:185-186 / 207-213):
@@ -60,8 +61,10 @@ enum { LS_ACT_NONE = 0, LS_ACT_GEGLU = 1, LS_ACT_GELU = 2, LS_ACT_SILU = 3 };
  * downsampler after F.pad(0,1,0,1); upsample = nearest x2 fused into the
  * gather (Upsample3D, resnet.py:53-73).
  *
- * Wp is the packed weight [N][K]: K = ksize*ksize*Cin rounded up to 64, tap-major
- * (see latentsync_amd/packing.py).  Epilogue, in this order:
+ * Wp is the packed weight [N][K]: K = ksize*ksize*Cin rounded up to 64, in the same
+ * k order: tap-major, except ksize 3 with Cin % 64 == 0, which is channel-chunk-major
+ * (the 9 taps of a 64-channel chunk consecutive; see latentsync_amd/packing.py).
+ * Epilogue, in this order:
  *   if (ln_rowstats)  acc = rstd[m] * (acc - mean[m] * ln_colsum[n])
  *       -- LayerNorm of the A rows folded into the GEMM: with Wp = W * gamma
  *       (per input column), bias = b + W beta and ln_colsum[n] = sum_k Wp[n, k],

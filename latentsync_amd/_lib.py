@@ -10,7 +10,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LS_HIP_LIB", os.path.join(HERE, "libls_hip.so"))
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 c_u16p = C.c_void_p
 c_vp = C.c_void_p

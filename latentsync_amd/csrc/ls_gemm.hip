@@ -34,7 +34,40 @@ struct ConvArgs {
   float* cs_out;  // GroupNorm column sums of y: [M / CS_ROWS][2][N] fp32 (sum, sum of squares per slot)
   int ablate;  // tuning only (bits): 2 = skip operand DMA, 4 = skip epilogue stores, 8 = skip epilogue,
                // 16 = skip MFMAs (DMA kernel)
+  int ccm;     // 3x3 with Cin % 64 == 0: K is channel-chunk-major, taps innermost (see tap_of)
+  int gm;      // tile raster: groups of gm row-blocks x all column tiles, row-block fastest (tile_of)
 };
+
+// Logical tile index -> (row-block, column-block), grouped: gm row-blocks x all ntn column
+// tiles per group, the row-block index fastest.  Tiles running together on an XCD (xcd_remap
+// gives every XCD a contiguous logical range) then share gm A row-bands and ~(concurrent /
+// gm) W column panels instead of one A band and a W panel per tile: the wide linears
+// (GEGLU W1, fused q|k|v) re-fetched their whole W per row-band (profiles/r03e_per_kernel.txt).
+// gm = 1 is the plain column-fastest order.
+__device__ __forceinline__ void tile_of(const ConvArgs& a, int bid, int& tm, int& tn) {
+  const int gsz = a.gm * a.ntn, g = bid / gsz, r = bid - g * gsz;
+  const int first = g * a.gm, rows = min(a.ntm - first, a.gm);
+  tm = first + r % rows;
+  tn = r / rows;
+}
+
+// K order of a 3x3 weight with Cin % 64 == 0 (packing.py): k = (ci / 64) * 576 + tap * 64 +
+// ci % 64 -- the 9 taps of one 64-channel chunk are consecutive K-tiles, so a block reads
+// a pixel chunk's 3x3 neighbourhood in 9 back-to-back K-tiles and the re-reads hit L2
+// (tap-major, the 9 re-reads of a pixel were Cin / 64 K-tiles apart and, with 64 blocks
+// per XCD streaming operands in between, missed: profiles/r03e_per_kernel.txt).
+// Returns the tap and sets c0 = the K-tile's first input channel (k0 = a 64-aligned or,
+// for BK 32, 32-aligned K offset).
+__device__ __forceinline__ int tap_of(const ConvArgs& a, int k0, int& c0) {
+  if (a.ccm) {
+    const int chunk = k0 / 576, rem = k0 - chunk * 576;
+    c0 = chunk * 64 + (rem & 63);
+    return rem >> 6;
+  }
+  const int tap = k0 / a.Cin;
+  c0 = k0 - tap * a.Cin;
+  return tap;
+}
 
 // ---------------------------------------------------------------- epilogue
 // Vectorised epilogue on 8 consecutive output columns (16-B bf16 / 32-B fp32
@@ -135,8 +168,8 @@ __device__ __forceinline__ uint4 load_a_chunk(const ConvArgs& a, int kt, int ch,
     c = kt * 64 + ch * 8;
     if (m >= a.M || c >= a.Cin) return make_uint4(0, 0, 0, 0);
   } else if (TAPU) {
-    tap = (kt * 64) / a.Cin;
-    c = kt * 64 - tap * a.Cin + ch * 8;
+    tap = tap_of(a, kt * 64, c);
+    c += ch * 8;
   } else {
     const int kc = kt * 8 + ch;
     tap = kc / a.CC;
@@ -484,7 +517,8 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvArgs a) {
   const int nt = a.ntm * a.ntn;
   const int z = bid / nt;
   bid -= z * nt;
-  const int tm = bid / a.ntn, tn = bid - tm * a.ntn;
+  int tm, tn;
+  tile_of(a, bid, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int kt0 = z * a.kt_per_split;
   const int kt1 = min(a.ktiles, kt0 + a.kt_per_split);
@@ -584,8 +618,8 @@ __device__ __forceinline__ const void* a_src(const ConvArgs& a, int kt, int c, i
     cg = kt * BK + c * 8;
     ok = (m < a.M) & (cg < a.Cin);
   } else if (TAPU) {
-    tap = (kt * BK) / a.Cin;
-    cg = kt * BK - tap * a.Cin + c * 8;
+    tap = tap_of(a, kt * BK, cg);
+    cg += c * 8;
     ok = true;
   } else {
     const int kc = kt * (BK / 8) + c;
@@ -718,10 +752,7 @@ struct BufDma {
       k.two = a.C2 && kt * 64 >= a.C1;  // concat: a K-tile lies in one source (host: C1 % 64 == 0)
       k.soff_a = k.two ? (kt * 64 - a.C1) * 2 : kt * 128;
     } else {
-      if (c0 == 0 && tap == 0 && kt != 0) {
-        tap = (kt * 64) / a.Cin;
-        c0 = kt * 64 - tap * a.Cin;
-      }
+      if (c0 == 0 && tap == 0 && kt != 0) tap = tap_of(a, kt * 64, c0);
       const int kh = tap / 3, kw = tap - kh * 3;
       k.tap = tap;
       k.two = c0 >= a.C1;
@@ -733,8 +764,12 @@ struct BufDma {
       } else {
         k.soff_a = ((kh * a.W + kw) * ld + (k.two ? c0 - a.C1 : c0)) * 2;
       }
-      c0 += 64;
-      if (c0 == a.Cin) { c0 = 0; ++tap; }
+      if (a.ccm) {
+        if (++tap == 9) { tap = 0; c0 += 64; }
+      } else {
+        c0 += 64;
+        if (c0 == a.Cin) { c0 = 0; ++tap; }
+      }
     }
     return k;
   }
@@ -794,7 +829,8 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_gemm_dma_kernel(ConvArgs a)
   int bid = xcd_remap(blockIdx.x, nt * a.split);
   const int z = bid / nt;
   bid -= z * nt;
-  const int tm = bid / a.ntn, tn = bid - tm * a.ntn;
+  int tm, tn;
+  tile_of(a, bid, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int ktiles = a.K / BK;
   const int kps = a.kt_per_split * (64 / BK);
@@ -949,7 +985,8 @@ __global__ void __launch_bounds__(512) conv_gemm_big_kernel(ConvArgs a) {
   int bid = xcd_remap(blockIdx.x, nt * a.split);
   const int z = bid / nt;
   bid -= z * nt;
-  const int tm = bid / a.ntn, tn = bid - tm * a.ntn;
+  int tm, tn;
+  tile_of(a, bid, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int kt0 = z * a.kt_per_split;
   const int kt1 = min(a.ktiles, kt0 + a.kt_per_split);
@@ -1098,7 +1135,8 @@ __global__ void __launch_bounds__(512) conv_gemm_p8_kernel(ConvArgs a) {
   int bid = xcd_remap(blockIdx.x, nt * a.split);
   const int z = bid / nt;
   bid -= z * nt;
-  const int tm = bid / a.ntn, tn = bid - tm * a.ntn;
+  int tm, tn;
+  tile_of(a, bid, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int kt0 = z * a.kt_per_split;
   const int nk = min(a.ktiles, kt0 + a.kt_per_split) - kt0;
@@ -1260,7 +1298,8 @@ __global__ void __launch_bounds__(512) conv_gemm_big4_kernel(ConvArgs a) {
   int bid = xcd_remap(blockIdx.x, nt * a.split);
   const int z = bid / nt;
   bid -= z * nt;
-  const int tm = bid / a.ntn, tn = bid - tm * a.ntn;
+  int tm, tn;
+  tile_of(a, bid, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int kps = a.kt_per_split * 2;  // 32-wide K-tiles per split
   const int kt0 = z * kps;
@@ -1794,6 +1833,9 @@ __global__ void __launch_bounds__(NW * 64, 2) gemm_rowblock_kernel(ConvArgs a) {
 
 // ---------------------------------------------------------------- host side
 static bool g_force_regstage = getenv("LS_GEMM_REGSTAGE") != nullptr;
+// A/B switch: 3x3 weights packed tap-major (packing.py reads the same variable)
+static const bool g_w3_tapmajor = getenv("LS_W3_TAPMAJOR") != nullptr;
+static const int g_gemm_gm = getenv("LS_GEMM_GM") ? atoi(getenv("LS_GEMM_GM")) : 0;  // A/B switch: tile raster
 static int g_force_tile = 0, g_force_split = 0, g_ablate = 0, g_bk = 64;
 
 struct TileCfg { int bm, bn, split; };
@@ -2128,6 +2170,8 @@ static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split
   if (a.cs_out && (M % CS_ROWS || d->N % 8 || d->ldy % 8 || d->act == LS_ACT_GEGLU || d->y_f32))
     return fail(LS_ERR_INVALID, "ls_conv2d: gn_colsum_out needs M % 128 == 0, N % 8 == 0, bf16 output, no GEGLU");
   a.ablate = g_ablate;
+  a.ccm = (d->ksize == 3 && Cin % 64 == 0 && !g_w3_tapmajor) ? 1 : 0;
+  a.gm = 1;  // (set with the tile below)
   a.ktiles = d->K / 64;
   t = pick_tile(M, d->N, a.ktiles, d->split_k <= 0 && d->workspace != nullptr,
                 !d->aff_scale && !g_force_regstage && (d->ksize == 1 || Cin % 64 == 0), d->ksize);
@@ -2137,6 +2181,10 @@ static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split
     t.bm = tb[g_force_tile][0]; t.bn = tb[g_force_tile][1]; t.split = g_force_split ? g_force_split : 1;
   }
   a.ntm = cdiv(M, t.bm > 256 ? 256 : t.bm); a.ntn = cdiv(d->N, t.bn);  // 257/258/259 = 256-row kernel variants
+  // grouped raster: ~32 (256-row, one block per CU) / 64 (128-row, two per CU) tiles run
+  // together per XCD -> 4 / 8 row-bands per group (LS_GEMM_GM overrides; 1 = column-fastest)
+  a.gm = g_gemm_gm > 0 ? g_gemm_gm : (t.bm >= 256 ? 4 : 8);
+  a.gm = std::max(1, std::min(a.gm, a.ntm));
   split = d->split_k > 0 ? d->split_k : t.split;
   split = std::min(split, a.ktiles);
   a.kt_per_split = cdiv(a.ktiles, split);
