@@ -1520,11 +1520,10 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
-template <int KT, int FM, int FN, int FLAGS, int NW = 8>
-__global__ void __launch_bounds__(NW * 64, 2) gemm_rowblock_kernel(ConvArgs a) {  // two waves per SIMD
+template <int KT, int FM, int FN, int FLAGS>
+__global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
   constexpr int BN = 16 * FN;
-  constexpr int NT = NW * 64;
-  constexpr int BM = NW * 16 * FM;            // rows per workgroup (NW waves x FM fragments of 16)
+  constexpr int BM = 8 * 16 * FM;             // rows per workgroup (8 waves x FM fragments of 16)
   constexpr int KTILES = KT / 2;              // 64-wide LDS images per chunk
   constexpr int WIMG = BN * KTILES * 8;       // uint4 of the W images of a chunk
   constexpr bool LN = FLAGS & RB_LN, RES = FLAGS & RB_RES, RV = FLAGS & RB_RV, GG = FLAGS & RB_GEGLU;
@@ -1532,12 +1531,8 @@ __global__ void __launch_bounds__(NW * 64, 2) gemm_rowblock_kernel(ConvArgs a) {
   // in flight two chunks ahead of its epilogue with no registers held (the register
   // residual, one chunk ahead, left the short-K residual GEMMs latency-bound on HBM)
   constexpr int RIMG = RES ? BM * BN / 8 : 0;  // uint4
-  constexpr int RPT = RIMG / NT;
-  // LDS: a 2-stage ring of W images (chunk c + 1 lands while chunk c computes) and a
-  // 3-stage ring of the chunks' column parameters (bias / colsum / row-vector columns,
-  // 3 x 64 fp32) + residual tiles, which live on until the chunk's epilogue one body later
-  constexpr int PST = 48 + RIMG;
-  constexpr int PBASE = 2 * WIMG;
+  constexpr int RPT = RIMG / 512;
+  constexpr int STAGE = WIMG + 48 + RIMG;     // + bias / colsum / row-vector columns (3 x 64 fp32) + residual
   constexpr bool AF = FLAGS & RB_AFF;  // GroupNorm affine (+SiLU) prologue on the register-resident A rows
   constexpr bool ST = (FLAGS & RB_STATS) && !GG;  // row statistics of the output (host: one N range per block)
   // GroupNorm column sums (a.cs_out): per chunk a wave's 16 FM rows are summed over its
@@ -1546,8 +1541,8 @@ __global__ void __launch_bounds__(NW * 64, 2) gemm_rowblock_kernel(ConvArgs a) {
   constexpr bool CS = (FLAGS & RB_GNCS) && !GG;
   constexpr int WPS = CS_ROWS / (16 * FM);  // waves per 128-row slot
   constexpr int NSTORE = GG ? FM * FN / 2 : FM * FN;
-  constexpr int PPT = (WIMG + NT - 1) / NT;   // 16-B DMA pieces per thread per chunk
-  static_assert(KT % 2 == 0 && WIMG % 256 == 0 && RIMG % NT == 0, "K must be a multiple of 64");
+  constexpr int PPT = (WIMG + 511) / 512;     // 16-B DMA pieces per thread per chunk
+  static_assert(KT % 2 == 0 && WIMG % 256 == 0, "K must be a multiple of 64");
   extern __shared__ __attribute__((aligned(16))) uint4 lds_dyn[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, lg = lane >> 4;
@@ -1556,31 +1551,29 @@ __global__ void __launch_bounds__(NW * 64, 2) gemm_rowblock_kernel(ConvArgs a) {
   const int c0 = (int)((long)nch * ns / a.ntn), c1 = (int)((long)nch * (ns + 1) / a.ntn);
   const int mw = rb * BM + wid * 16 * FM;  // this wave's first row
 
-  // chunk c -> W stage ws: W rows [BN c, BN c + BN) x all K as KTILES swizzled 64-wide
-  // images; parameter stage ps: the chunk's bias, colsum and row-vector values (wave 0)
-  // and its residual tile.
-  // piece q = p * NT + tid of a chunk's images: image t = q / (8 BN), row (q / 8) % BN, chunk q % 8
+  // chunk c -> LDS stage: W rows [64c, 64c + 64) x all K as KTILES swizzled 64-wide
+  // images, then the chunk's 64 bias, colsum and row-vector values (wave 0).
+  // piece q = p * 512 + tid of a chunk's images: image t = q / (8 BN), row (q / 8) % BN, chunk q % 8
   const long rv_base = RV ? rv_row(a, rb * BM) : 0;  // host: rows_per_vec % BM == 0
-  auto issue = [&](int c, int ws, int ps) {
-    uint4* dst = lds_dyn + ws * WIMG;
-    uint4* pdst = lds_dyn + PBASE + ps * PST;
+  auto issue = [&](int c, int stage) {
+    uint4* dst = lds_dyn + stage * STAGE;
 #pragma unroll
     for (int p = 0; p < PPT; ++p) {
-      const int q = p * NT + tid, t = q / (8 * BN), row = (q >> 3) % BN, pc = q & 7;
+      const int q = p * 512 + tid, t = q / (8 * BN), row = (q >> 3) % BN, pc = q & 7;
       const int lc = pc ^ ((row >> 1) & 7);  // logical 16-B chunk stored at physical chunk pc
-      if (WIMG % NT == 0 || q < WIMG)        // (wave-uniform)
-        glds16(a.w + (long)(c * BN + row) * a.K + t * 64 + lc * 8, dst + p * NT + wid * 64);
+      if (WIMG % 512 == 0 || q < WIMG)       // (wave-uniform)
+        glds16(a.w + (long)(c * BN + row) * a.K + t * 64 + lc * 8, dst + p * 512 + wid * 64);
     }
     if (wid == 0 && lane < 48 && (lane & 15) * 4 < BN) {
       const int q = lane >> 4, e = (lane & 15) * 4;
       const float* base = q == 0 ? a.bias : q == 1 ? nullptr : (RV ? a.rowvec + rv_base : nullptr);
-      const void* pv = base ? (const void*)(base + c * BN + e) : (const void*)ls_zero_page;
-      glds16(pv, pdst);
+      const void* ps = base ? (const void*)(base + c * BN + e) : (const void*)ls_zero_page;
+      glds16(ps, dst + WIMG);
     }
 #pragma unroll
     for (int p = 0; p < RPT; ++p) {  // residual piece q: row q / (BN / 8), 16-B column chunk q % (BN / 8)
-      const int q = p * NT + tid, row = q / (BN / 8), ch = q % (BN / 8);
-      glds16(a.res + (long)(rb * BM + row) * a.ldr + c * BN + ch * 8, pdst + 48 + p * NT + wid * 64);
+      const int q = p * 512 + tid, row = q / (BN / 8), ch = q % (BN / 8);
+      glds16(a.res + (long)(rb * BM + row) * a.ldr + c * BN + ch * 8, dst + WIMG + 48 + p * 512 + wid * 64);
     }
   };
 
@@ -1590,7 +1583,7 @@ __global__ void __launch_bounds__(NW * 64, 2) gemm_rowblock_kernel(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < FM; ++i) mrow[i] = *(const float2*)(a.ln_mr + 2L * (mw + i * 16 + l16));
   }
-  issue(c0, 0, 0);
+  issue(c0, 0);
   // A rows -> registers (B operand of C^T = W A^T: lane = row l16, k = 8 lg .. + 7 of each 32-wide step)
   bf16x8 ar[FM][KT];
 #pragma unroll
@@ -1648,7 +1641,7 @@ __global__ void __launch_bounds__(NW * 64, 2) gemm_rowblock_kernel(ConvArgs a) {
   // column parameters (bias + row vector) of chunk c from its LDS stage, read before
   // the next DMA is issued (an LDS read after it would wait for the DMA)
   auto load_prm = [&](int stage, float4 (&bb)[FN]) {
-    const float4* prm = (const float4*)(lds_dyn + PBASE + stage * PST);
+    const float4* prm = (const float4*)(lds_dyn + stage * STAGE + WIMG);
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       bb[j] = prm[lg + 4 * j];
@@ -1663,7 +1656,7 @@ __global__ void __launch_bounds__(NW * 64, 2) gemm_rowblock_kernel(ConvArgs a) {
   for (int i = 0; i < FM; ++i) { S1[i] = 0.0; S2[i] = 0.0; }
   auto epilogue = [&](int c, const float4 (&bb)[FN], f32x4 (&acc)[FM][FN], int stage) {
     const int nb = c * BN + 4 * lg;  // packed column of fragment j: nb + 16 j
-    const u16* rtile = (const u16*)(lds_dyn + PBASE + stage * PST + 48);  // [BM][BN] residual of chunk c
+    const u16* rtile = (const u16*)(lds_dyn + stage * STAGE + WIMG + 48);  // [BM][BN] residual of chunk c
     float cs1[FM], cs2[FM];  // this chunk's partial sums (fp32 over 4*FN values), folded into S in fp64
     float gcs[FM][FN][4];    // stored values of this chunk (CS)
 #pragma unroll
@@ -1715,7 +1708,7 @@ __global__ void __launch_bounds__(NW * 64, 2) gemm_rowblock_kernel(ConvArgs a) {
       for (int i = 0; i < FM; ++i) { S1[i] += (double)cs1[i]; S2[i] += (double)cs2[i]; }
     }
     if (CS) {  // column sums of this wave's rows -> LDS part[c & 1][wave][64]
-      float* part = (float*)(lds_dyn + PBASE + 3 * PST) + (c & 1) * NT + wid * 64;
+      float* part = (float*)(lds_dyn + 3 * STAGE) + (c & 1) * 512 + wid * 64;
       float mine = 0.f;
 #pragma unroll
       for (int v = 0; v < 16; ++v) {  // v = kind * 8 + j * 4 + r
@@ -1736,8 +1729,8 @@ __global__ void __launch_bounds__(NW * 64, 2) gemm_rowblock_kernel(ConvArgs a) {
   };
   // slots of this block's rows: add the WPS waves of each for chunk cc and write them
   auto merge_cs = [&](int cc) {
-    const float* part = (const float*)(lds_dyn + PBASE + 3 * PST) + (cc & 1) * NT;
-    for (int q = tid; q < (BM / CS_ROWS) * 64; q += NT) {
+    const float* part = (const float*)(lds_dyn + 3 * STAGE) + (cc & 1) * 512;
+    for (int q = tid; q < (BM / CS_ROWS) * 64; q += 512) {
       const int sl = q >> 6, e = q & 63;
       float t = 0.f;
 #pragma unroll
@@ -1747,7 +1740,7 @@ __global__ void __launch_bounds__(NW * 64, 2) gemm_rowblock_kernel(ConvArgs a) {
     }
   };
   auto mfma_chunk = [&](int stage, f32x4 (&acc)[FM][FN]) {
-    const uint4* cur = lds_dyn + stage * WIMG;
+    const uint4* cur = lds_dyn + stage * STAGE;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -1771,26 +1764,24 @@ __global__ void __launch_bounds__(NW * 64, 2) gemm_rowblock_kernel(ConvArgs a) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
-  // chunk c computes from W stage c % 2 while chunk c-1's parameters / residual stay in
-  // parameter stage (c-1) % 3 for its epilogue and chunk c+1 lands in W stage (c+1) % 2
-  // (chunk c-1's W: its MFMAs finished before the last barrier) and parameter stage
-  // (c+1) % 3.  Past the last chunk the DMA re-loads the last chunk into the spare
-  // stages, so the steady-state body is branch-free.
+  // 3-stage ring: chunk c computes from stage c%3 while chunk c-1's parameters stay in
+  // (c-1)%3 for its epilogue and chunk c+1 lands in (c+1)%3.  Past the last chunk the DMA
+  // re-loads the last chunk into the spare stage, so the steady-state body is branch-free.
+  // The residual tile of chunk c travels with the chunk's W images (stage c % 3).
   auto body = [&](int c, f32x4 (&acc)[FM][FN], f32x4 (&prev)[FM][FN]) {
     const int st = (c - c0) % 3;
     const int sp = st == 0 ? 2 : st - 1;
-    const int wst = (c - c0) & 1;
     float4 bb[FN];
     load_prm(sp, bb);
-    issue(min(c + 1, c1 - 1), wst ^ 1, st == 2 ? 0 : st + 1);
+    issue(min(c + 1, c1 - 1), st == 2 ? 0 : st + 1);
     if (CS && c - 2 >= c0) merge_cs(c - 2);  // written two epilogues ago, past a barrier
-    mfma_chunk(wst, acc);
+    mfma_chunk(st, acc);
     epilogue(c - 1, bb, prev, sp);
     wait_vm<NSTORE>();                                       // the DMA (older than the stores) landed
     sync();
   };
   // first chunk: no epilogue
-  issue(min(c0 + 1, c1 - 1), 1, 1);
+  issue(min(c0 + 1, c1 - 1), 1);
   mfma_chunk(0, acc0);
   wait_vm<0>();
   sync();
@@ -1885,19 +1876,14 @@ static bool g_rowblock = getenv("LS_GEMM_NO_ROWBLOCK") == nullptr;
 static bool g_rowblock640 = getenv("LS_GEMM_NO_ROWBLOCK640") == nullptr;
 static bool g_rb640_res = getenv("LS_GEMM_RB640_RES") != nullptr;  // A/B switch: K = 640 residual GEMMs too
 
-static int rowblock_nw(int K, int flags);
-// rows per row-block workgroup: NW waves x (K = 320: two, K = 640: one) 16-row fragments
-static int rowblock_bm(int K, int flags) { return rowblock_nw(K, flags) * 16 * (K == 320 ? 2 : 1); }
-static int rowblock_flags_of(const ConvArgs& a);
-
 static bool rowblock_ok(const ls_conv_desc* d, const ConvArgs& a) {
   if (!g_rowblock || g_force_tile || g_force_regstage || d->ksize != 1 || a.C2) return false;
   // GroupNorm affine prologue: one sample per block, and not together with the LayerNorm fold
-  if (a.aff_scale && (a.ln_mr || a.silu_in || a.pix_per_sample % rowblock_bm(a.Cin, rowblock_flags_of(a)) ||
+  if (a.aff_scale && (a.ln_mr || a.silu_in || a.pix_per_sample % (a.Cin == 320 ? 256 : 128) ||
                       ((uintptr_t)a.aff_scale | (uintptr_t)a.aff_shift) & 15))
     return false;
   // K = 640 only without a residual (the tiled kernel is faster there: 48 vs 53 us at 16x16)
-  if (!((a.Cin == 320 && a.K == 320 && a.M % rowblock_bm(320, rowblock_flags_of(a)) == 0) ||
+  if (!((a.Cin == 320 && a.K == 320 && a.M % 256 == 0) ||
         (g_rowblock640 && a.Cin == 640 && a.K == 640 && a.M % 128 == 0 && (!a.res || g_rb640_res))))
     return false;
   if (a.N % 64 || a.split != 1 || a.y_f32) return false;
@@ -1909,41 +1895,25 @@ static bool rowblock_ok(const ls_conv_desc* d, const ConvArgs& a) {
 
 // FN = 2 (32-column chunks): the FN = 4 variant needs > 256 VGPRs and spills, and a
 // spill's scratch traffic would break the kernel's counted vmcnt waits.
-// Wave count per block.  4-wave blocks of 128 rows run two per CU (67 KB of LDS each with
-// the residual ring), so one block's A-row load and stores can overlap the other's MFMAs.
-// Same-box A/B at 32 windows (profiles/r03d_rowblock_nw_ab.txt): the K = 320 GEGLU (LN
-// fold) 9.98 -> 9.61 ms per step with 4 waves, but the residual + row-statistics GEMMs
-// 5.41 -> 5.56 and the LN-folded q|k|v 3.40 -> 3.65 -- so only the GEGLU takes 4 waves.
-static const int g_rb_nw = getenv("LS_RB_NW") ? atoi(getenv("LS_RB_NW")) : 0;  // A/B switch: 4 / 8 for every K = 320
-static int rowblock_nw(int K, int flags) {
-  if (K != 320) return 8;
-  if (g_rb_nw == 4 || g_rb_nw == 8) return g_rb_nw;
-  return (flags & RB_GEGLU) ? 4 : 8;
-}
-
-template <int KT, int FM, int FLAGS, int NW>
+template <int KT, int FM, int FLAGS>
 static void launch_rowblock2(const ConvArgs& a, int grid, hipStream_t s) {
   constexpr int FN = 2;
-  constexpr int BM = NW * 16 * FM;
-  constexpr size_t WIMG = 16 * FN * (KT / 2) * 8, PST = 48 + ((FLAGS & RB_RES) ? BM * 16 * FN / 8 : 0);
-  const size_t shm = (2 * WIMG + 3 * PST) * 16 + ((FLAGS & RB_GNCS) ? 2 * NW * 64 * 4 : 0);
+  constexpr int BM = 8 * 16 * FM;
+  const size_t shm = (size_t)3 * (16 * FN * (KT / 2) * 8 + 48 + ((FLAGS & RB_RES) ? BM * 16 * FN / 8 : 0)) * 16 +
+                     ((FLAGS & RB_GNCS) ? 4096 : 0);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_rowblock_kernel<KT, FM, FN, FLAGS, NW>,
+    (void)hipFuncSetAttribute((const void*)gemm_rowblock_kernel<KT, FM, FN, FLAGS>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     attr = true;
   }
-  gemm_rowblock_kernel<KT, FM, FN, FLAGS, NW><<<grid, NW * 64, shm, s>>>(a);
+  gemm_rowblock_kernel<KT, FM, FN, FLAGS><<<grid, 512, shm, s>>>(a);
 }
 
 template <int FLAGS>
 static void launch_rowblock1(const ConvArgs& a, int grid, hipStream_t s) {
-  if (a.K == 320) {
-    if (rowblock_nw(320, FLAGS) == 4) launch_rowblock2<10, 2, FLAGS, 4>(a, grid, s);
-    else launch_rowblock2<10, 2, FLAGS, 8>(a, grid, s);
-  } else {
-    launch_rowblock2<20, 1, FLAGS, 8>(a, grid, s);
-  }
+  if (a.K == 320) launch_rowblock2<10, 2, FLAGS>(a, grid, s);
+  else launch_rowblock2<20, 1, FLAGS>(a, grid, s);
 }
 
 // returns false when no instance matches (the caller then uses the tiled kernels)
@@ -1953,19 +1923,15 @@ static const int kRowblockInstances[] = {0, RB_LN, RB_LN | RB_RV, RB_RES, RB_LN 
 
 // the row-block instance flags for this call, or -1; the row-block grid goes to
 // *ntm / *ntn only (the caller's tiled grid in a.ntm / a.ntn stays valid for a fallback)
-static int rowblock_flags_of(const ConvArgs& a) {
-  return (a.ln_mr ? RB_LN : 0) | (a.res ? RB_RES : 0) | (a.rowvec ? RB_RV : 0) | (a.act == LS_ACT_GEGLU ? RB_GEGLU : 0) |
-         (a.stats_out ? RB_STATS : 0) | (a.cs_out ? RB_GNCS : 0) | (a.aff_scale ? RB_AFF : 0);
-}
-
 static int rowblock_flags(const ConvArgs& a, int* ntm_out, int* ntn_out) {
-  const int flags = rowblock_flags_of(a);
-  const int bm = rowblock_bm(a.K, flags);
-  if (a.M % bm) return -1;
+  const int bm = a.K == 320 ? 256 : 128;
   const int ntm = a.M / bm, nch = a.N / 32;
   const int ntn = std::max(1, std::min(nch, (256 + ntm - 1) / ntm));
   if (a.stats_out && ntn != 1) return -1;  // fused statistics need whole rows per block
   if (a.cs_out && (bm % CS_ROWS || ntn != 1)) return -1;
+  const int flags = (a.ln_mr ? RB_LN : 0) | (a.res ? RB_RES : 0) | (a.rowvec ? RB_RV : 0) |
+                    (a.act == LS_ACT_GEGLU ? RB_GEGLU : 0) | (a.stats_out ? RB_STATS : 0) | (a.cs_out ? RB_GNCS : 0) |
+                    (a.aff_scale ? RB_AFF : 0);
   for (int f : kRowblockInstances)
     if (f == flags) {
       *ntm_out = ntm;
@@ -2181,9 +2147,11 @@ static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split
     t.bm = tb[g_force_tile][0]; t.bn = tb[g_force_tile][1]; t.split = g_force_split ? g_force_split : 1;
   }
   a.ntm = cdiv(M, t.bm > 256 ? 256 : t.bm); a.ntn = cdiv(d->N, t.bn);  // 257/258/259 = 256-row kernel variants
-  // grouped raster: ~32 (256-row, one block per CU) / 64 (128-row, two per CU) tiles run
-  // together per XCD -> 4 / 8 row-bands per group (LS_GEMM_GM overrides; 1 = column-fastest)
-  a.gm = g_gemm_gm > 0 ? g_gemm_gm : (t.bm >= 256 ? 4 : 8);
+  // grouped raster (LS_GEMM_GM=g, g row-bands per group): it cuts the wide linears' L2-miss
+  // fetch (GEGLU W1 at 8x8 3.6 -> 1.3 GB per call) but measured +0.4 ms per 32-window step
+  // against the column-fastest order over three alternated same-box rounds
+  // (profiles/r03i_locality_sweep.txt), so the default stays column-fastest (gm = 1)
+  a.gm = g_gemm_gm > 0 ? g_gemm_gm : 1;
   a.gm = std::max(1, std::min(a.gm, a.ntm));
   split = d->split_k > 0 ? d->split_k : t.split;
   split = std::min(split, a.ktiles);

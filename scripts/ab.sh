@@ -7,6 +7,7 @@
 # VARIANT  lib          A = latentsync_amd/libls_hip.so, B = latentsync_amd/libls_hip_ab.so
 #                       (build B with scripts/build_ab.sh COMMIT [file])
 #          env:VAR=VAL  A = plain, B = with VAR=VAL exported (an LS_* switch)
+#          lib+env:VAR=VAL  B = libls_hip_ab.so with VAR=VAL exported
 # MEASURE  step[:W]     scripts/step_ab.py, one graph-replayed UNet step at W windows (default 32)
 #          trace        rocprofv3 --kernel-trace of a 1-batch bench; per-kernel comparison of one
 #                       mid-run step (scripts/cmp_steps.py, min over runs) -> gpurun_out/TAG_cmp.txt
@@ -25,6 +26,7 @@ run() {  # $1 = A|B, $2 = round
   local envs=()
   case $variant in
     lib) [ "$1" = B ] && envs+=(LS_HIP_LIB=latentsync_amd/libls_hip_ab.so) ;;
+    lib+env:*) [ "$1" = B ] && envs+=(LS_HIP_LIB=latentsync_amd/libls_hip_ab.so "${variant#lib+env:}") ;;
     env:*) [ "$1" = B ] && envs+=("${variant#env:}") ;;
     *) echo "unknown variant $variant"; return 2 ;;
   esac
