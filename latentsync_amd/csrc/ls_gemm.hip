@@ -817,6 +817,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_gemm_dma_kernel(ConvArgs a)
   constexpr int FM = WTM / 16, FN = WTN / 16;
   constexpr int CPR = BK / 8;                         // 16-B chunks per row
   constexpr int AI = BM * CPR / NT, BI = BN * CPR / NT;  // DMA wave-instructions per wave per K-tile
+  static_assert((BM * CPR) % NT == 0 && (BN * CPR) % NT == 0, "operand pieces must divide over the threads");
   constexpr int L = AI + BI;
   constexpr int KSTEPS = BK / 32;
   constexpr int STAGE = (BM + BN) * CPR;              // uint4 per stage
@@ -2169,7 +2170,7 @@ using namespace ls;
 extern "C" int ls_set_tuning(int32_t key, int32_t value) {
   switch (key) {
     case 1: g_force_regstage = value != 0; return LS_OK;
-    case 2: if (value < 0 || value > 10) return fail(LS_ERR_INVALID, "tile id 0..10"); g_force_tile = value; return LS_OK;
+    case 2: if (value < 0 || value > 9) return fail(LS_ERR_INVALID, "tile id 0..9"); g_force_tile = value; return LS_OK;
     case 3: g_force_split = value; return LS_OK;
     case 4: g_ablate = value; return LS_OK;
     case 5: if (value != 32 && value != 64) return fail(LS_ERR_INVALID, "BK 32 or 64"); g_bk = value; return LS_OK;
@@ -2260,8 +2261,7 @@ extern "C" int ls_conv2d(const ls_conv_desc* d, void* stream) {
     else launch_big<128>(a, d->ksize, tapu, grid, s);
   } else if (t.bm == 128 && t.bn == 128) launch_cfg<128, 128, 2, 2>(a, d->ksize, tapu, grid, s);
   else if (t.bm == 128 && t.bn == 160) launch_cfg<128, 160, 2, 2>(a, d->ksize, tapu, grid, s);
-  else if (t.bm == 259 && t.bn == 160 && d->ksize == 3 && tapu && !a.aff_scale)
-    launch_dma1<256, 160, 4, 2, 3, true, 3, 64, EPI_ANY>(a, grid, s);  // 8-wave 3x3 tile, 3-stage ring
+
   else if (t.bm == 128 && t.bn == 64) launch_cfg<128, 64, 2, 2>(a, d->ksize, tapu, grid, s);
   else if (t.bm == 128 && t.bn == 32) launch_cfg<128, 32, 4, 1>(a, d->ksize, tapu, grid, s);
   else launch_cfg<64, 64, 2, 2>(a, d->ksize, tapu, grid, s);

@@ -41,7 +41,7 @@ run() {  # $1 = A|B, $2 = round
     *) echo "unknown measure $measure"; return 2 ;;
   esac
 }
-for r in 1 2; do
+for r in 1 2 3; do  # three alternated rounds: single-run A/Bs sit inside the +-1 % run-to-run spread
   for v in A B; do
     run $v $r || exit 1
   done
