@@ -2006,7 +2006,9 @@ static bool buf_dma_ok(const ConvArgs& a, int ks) {
 
 template <int BM, int BN, int WM, int WN, int KS, bool TAPU>
 static void launch_dma(const ConvArgs& a, int grid, hipStream_t s) {
-  if constexpr (BN >= 64) {
+  // (BK 32 tuning mode: only tiles whose 16-B operand pieces divide over the threads --
+  // 128 x 160 has 640 B pieces for 256 threads and would leave B rows unloaded)
+  if constexpr (BN >= 64 && (BN * 4) % (WM * WN * 64) == 0 && (BM * 4) % (WM * WN * 64) == 0) {
     if (g_bk == 32) { launch_dma1<BM, BN, WM, WN, KS, TAPU, 4, 32, EPI_ANY>(a, grid, s); return; }
   }
   if constexpr (KS == 1 || TAPU) {
