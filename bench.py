@@ -192,12 +192,22 @@ def step_probe(engine, device):
             blocks[-1][2] += fg + fa
         return r
 
-    ops.conv, ops.attention, ops.temporal_attention = conv, attention, temporal_attention
+    orig_ff = ops.feedforward
+
+    def feedforward(x2d, ln_stats, w1, w2, w2ff, out=None):
+        # fused LayerNorm + GEGLU W1 + W2 + residual (ls_feedforward): 2*M*2I*C + 2*M*C*I FLOPs
+        r = orig_ff(x2d, ln_stats, w1, w2, w2ff, out=out)
+        M, C = x2d.shape
+        if depth[0]:
+            blocks[-1][2] += 2.0 * M * w1.N * C + 2.0 * M * C * (w1.N // 2)
+        return r
+
+    ops.conv, ops.attention, ops.temporal_attention, ops.feedforward = conv, attention, temporal_attention, feedforward
     U._Transformer.__call__, U._Motion.__call__ = wrap(orig_t), wrap(orig_m)
     try:
         engine._step()
     finally:
-        ops.conv, ops.attention, ops.temporal_attention = orig_conv, orig_attn, orig_tattn
+        ops.conv, ops.attention, ops.temporal_attention, ops.feedforward = orig_conv, orig_attn, orig_tattn, orig_ff
         U._Transformer.__call__, U._Motion.__call__ = orig_t, orig_m
     torch.cuda.synchronize(device)
 

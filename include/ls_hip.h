@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LS_ABI_VERSION 10
+#define LS_ABI_VERSION 11
 
 typedef enum {
   LS_OK = 0,
@@ -244,6 +244,33 @@ typedef struct {
 } ls_tattn_desc;
 
 int ls_temporal_attention(const ls_tattn_desc* d, void* stream);
+
+/*
+ * FeedForward of a BasicTransformerBlock / TemporalTransformerBlock with its LayerNorm and
+ * residual, one launch (ABI 11; diffusers FeedForward(dim, "geglu"), attention.py:174-199
+ * norm3 + ff, motion_module.py:240-313 ff_norm + ff):
+ *   y = x + W2 (h * gelu_erf(g)) + b2,  [h | g] = W1 LN(x) + b1
+ * x, y: bf16 rows [M][ldx] / [M][ldy]; ln_rowstats: (mean, rstd) fp32 pairs of the x rows
+ * (the producing GEMM's row_stats_out); w1: bf16 [2*inner][C], the GEGLU rows interleaved
+ * in 16-row blocks (packing.geglu_interleave) with LayerNorm gamma folded in (W1 * gamma),
+ * b1: fp32 [2*inner] = b1 + W1 beta in the same order; w2: bf16 W2 [C][inner] re-packed
+ * per 32-column chunk (packing.pack_ff_w2: [inner/32][C][32], columns permuted and 16-B
+ * pieces swizzled to the kernel's register layout); b2: fp32 [C].  C = 320, inner = 1280
+ * (the 32x32 level) only.  The 4C-wide GEGLU intermediate never reaches memory.
+ */
+typedef struct {
+  const void* x;
+  const float* ln_rowstats;
+  const void* w1;
+  const float* b1;
+  const void* w2;
+  const float* b2;
+  void* y;
+  int64_t M;
+  int32_t ldx, ldy, C, inner;
+} ls_ff_desc;
+
+int ls_feedforward(const ls_ff_desc* d, void* stream);
 
 /*
  * Small-M linear in fp32: y[m, n] = sum_k act(x[m, k]) * W[n, k] + bias[n]

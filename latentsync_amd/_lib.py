@@ -10,7 +10,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LS_HIP_LIB", os.path.join(HERE, "libls_hip.so"))
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 c_u16p = C.c_void_p
 c_vp = C.c_void_p
@@ -54,6 +54,12 @@ class TAttnDesc(C.Structure):
                 ("F", C.c_int32), ("S", C.c_int32), ("eps", C.c_float)]
 
 
+class FFDesc(C.Structure):
+    _fields_ = [("x", c_vp), ("ln_rowstats", c_vp), ("w1", c_vp), ("b1", c_vp), ("w2", c_vp), ("b2", c_vp),
+                ("y", c_vp), ("M", C.c_int64), ("ldx", C.c_int32), ("ldy", C.c_int32), ("C", C.c_int32),
+                ("inner", C.c_int32)]
+
+
 _SIGS = {
     "ls_abi_version": (C.c_int, []),
     "ls_last_error": (C.c_char_p, []),
@@ -75,6 +81,7 @@ _SIGS = {
     "ls_attention_fp8_workspace_bytes": (C.c_size_t, [C.POINTER(AttnDesc)]),
     "ls_attention_fp8": (C.c_int, [C.POINTER(AttnDesc), c_vp, C.c_size_t, c_vp]),
     "ls_temporal_attention": (C.c_int, [C.POINTER(TAttnDesc), c_vp]),
+    "ls_feedforward": (C.c_int, [C.POINTER(FFDesc), c_vp]),
     "ls_small_linear": (C.c_int, [c_vp, C.c_int32, C.c_int32, c_vp, c_vp, C.c_int32, C.c_int32, c_vp, c_vp]),
     "ls_timestep_embed": (C.c_int, [c_vp, c_vp, C.c_int32, C.c_int32, C.c_int32, C.c_float, c_vp, c_vp]),
     "ls_ddim_cfg_step": (C.c_int, [c_vp, C.c_int32, C.c_int32, C.c_int64, C.c_float, c_vp, c_vp, c_vp, c_vp,

@@ -1,0 +1,211 @@
+// FeedForward of BasicTransformerBlock / TemporalTransformerBlock at C = 320 fused into
+// one gfx950 kernel (diffusers FeedForward(dim, activation_fn="geglu"): GEGLU proj
+// C -> 2*4C, h * gelu(g), Linear 4C -> C; attention.py:174-199 norm3 + ff,
+// motion_module.py:240-313 ff_norm + ff), with the LayerNorm folded in and the
+// residual added:
+//
+//   y = x + W2 GEGLU(W1 LN(x) + b1) + b2
+//
+// Before this kernel the 4C-wide GEGLU output went to HBM and came back (1.3 GB each
+// way per call at 32 windows): the W1 row-block GEMM (VALU-bound on its GELU epilogue)
+// and the W2 tiled GEMM (memory-bound) ran 1.0 + 0.59 ms.
+//
+// A workgroup owns 128 rows (8 waves x 16); a wave keeps its 16 rows of LN(x) in
+// registers (40 VGPRs; LayerNorm applied in place from the producer's row statistics,
+// gamma / beta folded into W1 / b1 on the host) and the C^T = W2 G^T accumulator of all C
+// output columns (20 tiles, 80 VGPRs).  The inner dimension streams in chunks of 32
+// GEGLU columns: per chunk the 64 interleaved W1 rows (h, g tiles, 40 KB) and the W2
+// columns (C x 32, 20 KB) arrive by LDS DMA into one of two stages while the previous
+// chunk computes:
+//   * GEMM1: C^T = W1 A^T (16x16x32), four 16-row tiles h0 g0 h1 g1 -- a lane holds 4
+//     consecutive GEGLU columns of its row in each;
+//   * GEGLU on the accumulators -> 8 bf16 per lane: columns 4 lg .. + 3 and 16 + 4 lg .. + 3
+//     of the chunk;
+//   * GEMM2: those 8 values ARE the B operand of out^T += W2 G^T for k-slots lg*8 .. + 7,
+//     because the host packs each W2 chunk with its 32 columns permuted the same way
+//     (slot (lg, i) -> column i < 4 ? 4 lg + i : 16 + 4 lg + i - 4): the intermediate
+//     never leaves the registers.
+// W2 chunk images are [C rows][4 x 16 B] with the 16-B pieces XOR-swizzled by
+// ((row >> 3) & 1) << 1 (host-side), which makes every ds_read_b128 lane group hit
+// 64 distinct banks; W1 images use the row-block kernel's 64-wide swizzle.
+#include "ls_common.h"
+
+namespace ls {
+
+struct FFArgs {
+  const u16* x;       // [M][ldx] FF input (pre-LayerNorm), also the residual
+  const float* ln_mr; // [M][2] (mean, rstd) of x rows
+  const u16* w1;      // [2I][C] GEGLU W1, rows interleaved in 16-blocks (h, g), LN gamma folded
+  const float* b1;    // [2I] its bias (+ W1 beta), same interleave
+  const u16* w2;      // [I/32][C][32] W2 chunks, columns permuted + pieces swizzled (see above)
+  const float* b2;    // [C]
+  u16* y;             // [M][ldy]
+  long M;
+  int ldx, ldy;
+};
+
+template <int C, int I, int PD1 = 2, int PD2 = 6>
+__global__ void __launch_bounds__(512, 1) ff_fused_kernel(FFArgs a) {
+  constexpr int KT = C / 32;              // GEMM1 k-steps
+  constexpr int NCH = I / 32;             // inner chunks
+  constexpr int WIMG = 64 * (C / 64) * 8; // uint4: W1 chunk, C/64 images of [64 rows][8 pieces]
+  constexpr int W2IMG = C * 4;            // uint4: W2 chunk, [C rows][4 pieces]
+  constexpr int STAGE = WIMG + W2IMG;
+  constexpr int NT2 = C / 16;             // output tiles
+  constexpr int PW1 = WIMG / 512;         // W1 pieces per thread per chunk
+  constexpr int UW2 = W2IMG / 64;         // W2 wave-instructions per chunk
+  static_assert(WIMG % 512 == 0 && W2IMG % 64 == 0 && C % 64 == 0 && I % 32 == 0, "ff_fused shape");
+  static_assert(PD1 >= 1 && PD1 <= KT && PD2 >= PD1 && PD2 <= NT2, "prefetch depths");
+  extern __shared__ __attribute__((aligned(16))) uint4 lds[];  // [2][STAGE], then b1 (2I fp32)
+  float* b1s = (float*)(lds + 2 * STAGE);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l16 = lane & 15, lg = lane >> 4;
+  const long row = (long)blockIdx.x * 128 + wid * 16 + l16;
+  const bool live = row < a.M;
+
+  for (int i = tid; i < 2 * I / 4; i += 512) ((float4*)b1s)[i] = ((const float4*)a.b1)[i];
+
+  auto issue = [&](int c, int st) {
+    uint4* dst = lds + st * STAGE;
+#pragma unroll
+    for (int p = 0; p < PW1; ++p) {  // piece q: image p (k 64p .. 64p + 63), row (q / 8) % 64, physical chunk q % 8
+      const int q = p * 512 + tid, r = (q >> 3) & 63, pc = q & 7;
+      const int lc = pc ^ ((r >> 1) & 7);
+      glds16(a.w1 + (long)(c * 64 + r) * C + p * 64 + lc * 8, dst + p * 512 + wid * 64);
+    }
+    for (int u = wid; u < UW2; u += 8)  // W2 chunk: a contiguous copy (host-packed layout)
+      glds16(a.w2 + ((long)c * W2IMG + u * 64 + lane) * 8, dst + WIMG + u * 64);
+  };
+  issue(0, 0);
+
+  // A rows -> registers, LayerNorm in place (bf16, like the reference's normalised rows)
+  bf16x8 ar[KT];
+  {
+    const u16* src = a.x + (live ? row : 0) * a.ldx + lg * 8;
+#pragma unroll
+    for (int s = 0; s < KT; ++s) ar[s] = live ? *(const bf16x8*)(src + s * 32) : __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0));
+    const float2 mr = live ? *(const float2*)(a.ln_mr + 2 * row) : make_float2(0.f, 0.f);
+    const float rstd = mr.y, nmr = -mr.x * mr.y;
+#pragma unroll
+    for (int s = 0; s < KT; ++s) {
+      bf16x8 v = ar[s];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (__bf16)fmaf((float)v[e], rstd, nmr);
+      ar[s] = v;
+    }
+  }
+
+  f32x4 out[NT2];
+#pragma unroll
+  for (int t = 0; t < NT2; ++t) out[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int p2 = lg ^ (((l16 >> 3) & 1) << 1);  // this lane's physical W2 piece
+
+  for (int c = 0; c < NCH; ++c) {
+    wait_vm<0>();  // this wave's DMA of chunk c (and the A rows) landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // everyone's; the other stage (chunk c - 1) is no longer read
+    asm volatile("" ::: "memory");
+    if (c + 1 < NCH) issue(c + 1, (c + 1) & 1);
+    const uint4* cur = lds + (c & 1) * STAGE;
+
+    // GEMM1: the chunk's 4 W1 tiles (h0 g0 h1 g1)
+    f32x4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    auto frag = [&](int s, int t) {
+      return __builtin_bit_cast(bf16x8, cur[(s >> 1) * 512 + swz_bk<64>(t * 16 + l16, (s & 1) * 4 + lg)]);
+    };
+    // W1 fragments PD1 k-steps ahead, the first PD2 W2 fragments issued under GEMM1 (an
+    // LDS read one MFMA ahead left each W2 MFMA waiting out the read's latency)
+    const uint4* w2 = cur + WIMG;
+    bf16x8 wf[PD1][4];
+#pragma unroll
+    for (int p = 0; p < PD1; ++p)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) wf[p][t] = frag(p, t);
+    uint4 w2q[PD2];
+#pragma unroll
+    for (int s = 0; s < KT; ++s) {
+      const int sl = s % PD1;
+      bf16x8 cw[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) cw[t] = wf[sl][t];
+      if (s + PD1 < KT) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) wf[sl][t] = frag(s + PD1, t);
+      } else if (s + PD1 - KT < PD2) {
+        w2q[s + PD1 - KT] = w2[((s + PD1 - KT) * 16 + l16) * 4 + p2];
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cw[t], ar[s], acc[t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = PD1; q < PD2; ++q) w2q[q] = w2[(q * 16 + l16) * 4 + p2];
+    // GEGLU -> the B operand of GEMM2 (k-slot order matches the host's W2 permutation)
+    const float* bb = b1s + c * 64 + 4 * lg;
+    const float4 bh0 = *(const float4*)(bb), bg0 = *(const float4*)(bb + 16);
+    const float4 bh1 = *(const float4*)(bb + 32), bg1 = *(const float4*)(bb + 48);
+    const float hb0[4] = {bh0.x, bh0.y, bh0.z, bh0.w}, gb0[4] = {bg0.x, bg0.y, bg0.z, bg0.w};
+    const float hb1[4] = {bh1.x, bh1.y, bh1.z, bh1.w}, gb1[4] = {bg1.x, bg1.y, bg1.z, bg1.w};
+    bf16x8 gv;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      gv[r] = (__bf16)((acc[0][r] + hb0[r]) * gelu_erf(acc[1][r] + gb0[r]));
+      gv[4 + r] = (__bf16)((acc[2][r] + hb1[r]) * gelu_erf(acc[3][r] + gb1[r]));
+    }
+    // GEMM2: out^T[16 t + 4 lg + r][row] += W2[16 t + l16][chunk k-slots] . G^T, W2
+    // fragments PD2 tiles ahead
+#pragma unroll
+    for (int t = 0; t < NT2; ++t) {
+      const bf16x8 wv = __builtin_bit_cast(bf16x8, w2q[t % PD2]);
+      if (t + PD2 < NT2) w2q[t % PD2] = w2[((t + PD2) * 16 + l16) * 4 + p2];
+      out[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, gv, out[t], 0, 0, 0);
+    }
+  }
+
+  // y = out + b2 + x (the residual: FF input rows, re-read -- the registers hold LN(x))
+  if (live) {
+    const u16* xr = a.x + row * a.ldx;
+    u16* yr = a.y + row * a.ldy;
+#pragma unroll
+    for (int t = 0; t < NT2; ++t) {
+      const int col = 16 * t + 4 * lg;
+      const float4 b = *(const float4*)(a.b2 + col);
+      const uint2 rs = *(const uint2*)(xr + col);
+      const float o0 = out[t][0] + b.x + __uint_as_float(rs.x << 16);
+      const float o1 = out[t][1] + b.y + __uint_as_float(rs.x & 0xffff0000u);
+      const float o2 = out[t][2] + b.z + __uint_as_float(rs.y << 16);
+      const float o3 = out[t][3] + b.w + __uint_as_float(rs.y & 0xffff0000u);
+      *(uint2*)(yr + col) = make_uint2(pack2(o0, o1), pack2(o2, o3));
+    }
+  }
+}
+
+}  // namespace ls
+
+using namespace ls;
+
+extern "C" int ls_feedforward(const ls_ff_desc* d, void* stream) {
+  if (!d || !d->x || !d->ln_rowstats || !d->w1 || !d->b1 || !d->w2 || !d->b2 || !d->y)
+    return fail(LS_ERR_INVALID, "ls_feedforward: null pointer");
+  if (d->C != 320 || d->inner != 1280) return fail(LS_ERR_INVALID, "ls_feedforward: C = 320, inner = 1280 only");
+  if (d->M <= 0 || d->ldx < d->C || d->ldy < d->C || d->ldx % 8 || d->ldy % 4)
+    return fail(LS_ERR_INVALID, "ls_feedforward: bad rows / pitches (ldx % 8, ldy % 4, >= C)");
+  if ((((uintptr_t)d->x | (uintptr_t)d->w1 | (uintptr_t)d->w2 | (uintptr_t)d->b1 | (uintptr_t)d->b2) & 15) ||
+      (((uintptr_t)d->y | (uintptr_t)d->ln_rowstats) & 7))
+    return fail(LS_ERR_INVALID, "ls_feedforward: x / w1 / w2 / b1 / b2 16-B aligned, y / ln_rowstats 8-B aligned");
+  if ((d->M + 127) / 128 > 0x7fffffffL) return fail(LS_ERR_INVALID, "ls_feedforward: too many rows");
+  FFArgs a;
+  a.x = (const u16*)d->x; a.ln_mr = d->ln_rowstats; a.w1 = (const u16*)d->w1; a.b1 = d->b1;
+  a.w2 = (const u16*)d->w2; a.b2 = d->b2; a.y = (u16*)d->y; a.M = d->M; a.ldx = d->ldx; a.ldy = d->ldy;
+  constexpr int C = 320, I = 1280;
+  const size_t shm = (size_t)2 * (64 * (C / 64) * 8 + C * 4) * 16 + 2 * I * sizeof(float);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)ff_fused_kernel<C, I>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    attr = true;
+  }
+  ff_fused_kernel<C, I><<<(unsigned)((d->M + 127) / 128), 512, shm, (hipStream_t)stream>>>(a);
+  return check_launch("ff_fused_kernel");
+}

@@ -312,6 +312,28 @@ def temporal_attention(x2d, pk: TemporalPack, n_samples, F, S, out=None):
     return out
 
 
+def feedforward_ok(x2d, w1: "Packed", w2: "Packed"):
+    """Shapes ls_feedforward takes (else the GEGLU row-block GEMM + the W2 GEMM)."""
+    return (x2d.shape[1] == 320 and w1.N == 2560 and w1.K == 320 and w1.geglu and w2.N == 320 and w2.K == 1280
+            and x2d.stride(1) == 1 and x2d.stride(0) % 8 == 0)
+
+
+def feedforward(x2d, ln_stats, w1: "Packed", w2: "Packed", w2ff, out=None):
+    """y = x + W2 GEGLU(W1 LN(x) + b1) + b2 in one launch (ls_feedforward): x2d (M, 320)
+    rows, ln_stats (M, 2) their (mean, rstd); w1 the LN-folded GEGLU operand, w2 the W2
+    operand (bias), w2ff = packing.pack_ff_w2(W2) bf16."""
+    lib = _lib.load()
+    M, C_ = x2d.shape
+    if out is None:
+        out = torch.empty((M, C_), dtype=torch.bfloat16, device=x2d.device)
+    d = _lib.FFDesc()
+    d.x, d.ln_rowstats, d.w1, d.b1 = _p(x2d), _p(ln_stats), _p(w1.w), _p(w1.bias)
+    d.w2, d.b2, d.y = _p(w2ff), _p(w2.bias), _p(out)
+    d.M, d.ldx, d.ldy, d.C, d.inner = M, x2d.stride(0), out.stride(0), C_, w1.N // 2
+    check(lib.ls_feedforward(C.byref(d), _stream()), "ls_feedforward")
+    return out
+
+
 def attention_fp8_workspace_bytes(*, batch, heads, nk, head_dim):
     lib = _lib.load()
     d = _lib.AttnDesc()

@@ -72,3 +72,20 @@ def geglu_interleave(w1: torch.Tensor, b1: torch.Tensor):
     bh, bg = b1[:n2], b1[n2:]
     b = torch.stack([bh.reshape(-1, 16), bg.reshape(-1, 16)], 1).reshape(-1)
     return w, b
+
+
+def pack_ff_w2(w2: torch.Tensor) -> torch.Tensor:
+    """FeedForward W2 (C, I) -> [I/32][C][32] for ls_feedforward (include/ls_hip.h): per
+    32-column chunk, k-slot (lg, i) of a row holds column i < 4 ? 4 lg + i : 16 + 4 lg + i - 4
+    (the GEGLU values a lane holds after GEMM1), and the row's four 16-B pieces are stored
+    at physical piece lg ^ (((row >> 3) & 1) << 1) (conflict-free ds_read_b128)."""
+    C, I = w2.shape
+    assert I % 32 == 0
+    perm = torch.tensor([(4 * lg + i) if i < 4 else (16 + 4 * lg + i - 4) for lg in range(4) for i in range(8)])
+    w = w2.float().reshape(C, I // 32, 32)[:, :, perm]          # (C, chunk, 32 logical slots)
+    w = w.reshape(C, I // 32, 4, 8)                              # (..., logical piece, 8)
+    rows = torch.arange(C)
+    phys = torch.arange(4)[None, :] ^ (((rows[:, None] >> 3) & 1) << 1)  # logical -> physical piece
+    out = torch.empty_like(w)
+    out[rows[:, None], :, phys, :] = w.permute(0, 2, 1, 3)       # (C, piece, chunk, 8) scattered
+    return out.permute(1, 0, 2, 3).reshape(I // 32, C, 32).contiguous()

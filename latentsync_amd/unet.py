@@ -29,12 +29,31 @@ import torch
 
 from . import ops
 from .config import STAGE2_MODEL
-from .packing import geglu_interleave, pack_weight, pad_bias
+from .packing import geglu_interleave, pack_ff_w2, pack_weight, pad_bias
 from .schema import unet_param_shapes
 from .weights import fill_state_dict
 
 # LS_FUSED_TEMPORAL=0: the motion attention as q|k|v GEMM + ls_attention (A/B switch)
 _FUSED_TEMPORAL = os.environ.get("LS_FUSED_TEMPORAL", "1") != "0"
+# LS_FUSED_FF=0: the FeedForward as GEGLU row-block GEMM + W2 GEMM (A/B switch)
+_FUSED_FF = os.environ.get("LS_FUSED_FF", "1") != "0"
+
+
+def _ff(h, st, ff1, ff2, ff2p):
+    """norm + FeedForward + residual: ls_feedforward at C = 320 (the GEGLU intermediate
+    stays in registers), else the GEGLU GEMM (LN folded) and the W2 GEMM with the residual."""
+    if ff2p is not None and ops.feedforward_ok(h, ff1, ff2):
+        return ops.feedforward(h, st, ff1, ff2, ff2p)
+    g = ops.linear(h, ff1, act=ops.ACT_GEGLU, ln_stats=st)
+    return ops.linear(g, ff2, res=h)
+
+
+def _ff2_packed(dv, key):
+    """W2 of a C = 320 FeedForward re-packed for ls_feedforward (packing.pack_ff_w2)."""
+    w = dv.sd[key]
+    if not _FUSED_FF or tuple(w.shape) != (320, 1280):
+        return None
+    return pack_ff_w2(w.float().cpu()).to(torch.bfloat16).to(dv.device).contiguous()
 
 _DEFAULTS = dict(
     sample_size=None, in_channels=4, out_channels=4, center_input_sample=False, flip_sin_to_cos=True, freq_shift=0,
@@ -163,6 +182,7 @@ class _Transformer:
         self.ff1 = dv.packed_ln(sd[b + ".ff.net.0.proj.weight"], sd[b + ".ff.net.0.proj.bias"], ln(b + ".norm3"),
                                 geglu=True)
         self.ff2 = dv.packed(b + ".ff.net.2.weight", b + ".ff.net.2.bias")
+        self.ff2p = _ff2_packed(dv, b + ".ff.net.2.weight")
 
     def audio_kv(self, audio_rows):
         """The audio cross-attention k|v projection (attn2.to_k / to_v of the audio
@@ -199,8 +219,7 @@ class _Transformer:
                           os_=(HW * C, 0, C, d))
             h = ops.linear(o, self.o2, res=h, stats_out=st)
         # GEGLU feed-forward (norm3 folded)
-        g = ops.linear(h, self.ff1, act=ops.ACT_GEGLU, ln_stats=st)
-        h = ops.linear(g, self.ff2, res=h)
+        h = _ff(h, st, self.ff1, self.ff2, self.ff2p)
         return ops.conv(h.view(n, H, W, C), self.proj_out, res=x, gn_out=True)
 
 
@@ -236,6 +255,7 @@ class _Motion:
         self.ff1 = dv.packed_ln(sd[b + ".ff.net.0.proj.weight"], sd[b + ".ff.net.0.proj.bias"],
                                 (sd[b + ".ff_norm.weight"], sd[b + ".ff_norm.bias"]), geglu=True)
         self.ff2 = dv.packed(b + ".ff.net.2.weight", b + ".ff.net.2.bias")
+        self.ff2p = _ff2_packed(dv, b + ".ff.net.2.weight")
 
     def __call__(self, x, B):
         n, H, W, C = x.shape
@@ -263,8 +283,7 @@ class _Motion:
                 ops.attention(qkv, qkv[:, C:], qkv[:, 2 * C:], o, batch=B * S, z2=S, heads=self.heads, nq=F, nk=F,
                               head_dim=d, qs=st, ks=st, vs=st, os_=(F * S * C, C, S * C, d))
             h = ops.linear(o, a["o"], res=h, stats_out=lns)
-        g = ops.linear(h, self.ff1, act=ops.ACT_GEGLU, ln_stats=lns)
-        h = ops.linear(g, self.ff2, res=h)
+        h = _ff(h, lns, self.ff1, self.ff2, self.ff2p)
         return ops.conv(h.view(n, H, W, C), self.proj_out, res=x, gn_out=True)
 
 

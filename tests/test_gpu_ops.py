@@ -557,3 +557,31 @@ def test_gn_affine_fold(gpu, K, M, N, H, silu):
     d.w, d.K, d.N, d.y, d.ldy = pw.w.data_ptr(), pw.K, pw.N, y1.data_ptr(), N
     d.row_stats_out = st1.data_ptr()
     assert _lib.load().ls_conv_path(ctypes.byref(d)) == (1 if K in (320, 640) else 2)
+
+
+@pytest.mark.parametrize("M", [128, 1000, 8192])
+def test_feedforward_fused(gpu, M):
+    """ls_feedforward (C = 320): y = x + W2 GEGLU(W1 LN(x) + b1) + b2 against the fp32
+    reference (diffusers FeedForward / GEGLU after nn.LayerNorm, attention.py:174-199),
+    ragged row counts, and against the unfused path (GEGLU row-block GEMM + W2 GEMM)."""
+    from latentsync_amd.unet import _Dev, _ff
+    from latentsync_amd.packing import pack_ff_w2
+    C, I = 320, 1280
+    x = bf(rnd(M, C, seed=80) * 2 + 0.5)
+    gamma, beta = 1 + 0.2 * rnd(C, seed=81), 0.1 * rnd(C, seed=82)
+    w1, b1 = rnd(2 * I, C, seed=83, scale=1 / math.sqrt(C)), rnd(2 * I, seed=84, scale=0.1)
+    w2, b2 = rnd(C, I, seed=85, scale=1 / math.sqrt(I)), rnd(C, seed=86, scale=0.1)
+    xn = F.layer_norm(x, (C,), gamma, beta, eps=1e-5)
+    hg = xn @ w1.T + b1
+    ref = x + (hg[:, :I] * F.gelu(hg[:, I:])) @ w2.T + b2
+    dv = _Dev({"w2": w2, "b2": b2}, DEV)
+    ff1 = dv.packed_ln(w1, b1, (gamma, beta), geglu=True)
+    ff2 = dv.packed("w2", "b2")
+    ff2p = pack_ff_w2(w2).to(torch.bfloat16).to(DEV)
+    xd = x.to(torch.bfloat16).to(DEV)
+    st = ops.row_stats(xd)
+    assert ops.feedforward_ok(xd, ff1, ff2)
+    y = ops.feedforward(xd, st, ff1, ff2, ff2p).float().cpu()
+    y2 = _ff(xd, st, ff1, ff2, None).float().cpu()
+    assert rel_err(y - x, ref - x) < 2e-2
+    assert rel_err(y, y2) < 1e-2
