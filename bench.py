@@ -54,9 +54,12 @@ PEAK_BF16_TF = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 # plumbing case, configs[3] is configs[1] sharded over 8 ranks)
 # windows: independent 16-frame windows of a clip batched per UNet call (measured on MI355X:
 # 8 -> 110.2, 16 -> 113.3 frames/s at configs[1], profiles/r01f_bench.json; same box, round 2
-# (profiles/r02k_wpb_sweep.txt): 16 -> 121.4, 24 -> 122.9, 32 -> 123.2; configs[4] 2 -> 27.3, 4 -> 28.1)
+# (profiles/r02k_wpb_sweep.txt): 16 -> 121.4, 24 -> 122.9, 32 -> 123.2; configs[4] 2 -> 27.3, 4 -> 28.1;
+# round 3, after the kernel changes (profiles/r03p_wpb_sweep.txt, two boxes, two rounds each):
+# 24 -> 130.0-130.4, 32 -> 129.5, 48 -> 130.6-130.7 on one, 40 -> 133.9-134.4, 48 -> 135.0-135.8,
+# 56 -> 134.4-135.0, 64 -> 135.2-135.6 on the other)
 PRESETS = {
-    1: dict(resolution=256, guidance=1.0, steps=20, windows=32),
+    1: dict(resolution=256, guidance=1.0, steps=20, windows=48),
     2: dict(resolution=256, guidance=2.0, steps=50, windows=8),
     # configs[4] names "fp8 MFMA attention": ls_attention_fp8 (P.V on the block-scaled e4m3
     # MFMA) is built and parity-tested, but measured no faster than bf16 on the same box

@@ -1,9 +1,9 @@
 # Two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE -- separate runs, TCC slots) of a
 # short eager bench, then the per-ls_conv2d-call HBM traffic -> profiles/pmc_traffic.json
-# usage: bash scripts/pmc_pass.sh TAG [windows per UNet call, default 32 = bench.py's configs[1]]
+# usage: bash scripts/pmc_pass.sh TAG [windows per UNet call, default 48 = bench.py's configs[1]]
 set -o pipefail
 tag=${1:-pmc}
-nw=${2:-32}
+nw=${2:-48}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 B="scripts/pmc_step.py $nw 3"
