@@ -11,6 +11,7 @@ import shutil
 import subprocess
 import sys
 import tempfile
+import warnings
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
@@ -55,7 +56,8 @@ def _spills(stderr):
 
 
 OBJDUMP = os.environ.get("LLVM_OBJDUMP", "/opt/rocm/lib/llvm/bin/llvm-objdump")
-_PK_OPSEL = re.compile(r"v_pk_(?:fma|mul|add)_f32\b[^\n]*\bop_sel:\[([01,]+)\]")
+# every packed-fp32 VALU opcode (v_pk_fma/mul/add/mov_f32 ...), any op_sel bit set
+_PK_OPSEL = re.compile(r"v_pk_\w+_f32\b[^\n]*\bop_sel:\[([01,]+)\]")
 
 
 def _packed_opsel(obj):
@@ -69,7 +71,10 @@ def _packed_opsel(obj):
         r = subprocess.run([OBJDUMP, "--offloading", cp], capture_output=True, text=True, cwd=td)
         dev = [f for f in os.listdir(td) if "gfx950" in f]
         if r.returncode != 0 or not dev:
-            raise RuntimeError(f"could not extract the gfx950 code object of {obj}: {r.stderr}")
+            # an llvm-objdump without --offloading: skip the guard as for a missing objdump
+            warnings.warn(f"packed-fp32 op_sel guard skipped: could not extract the gfx950 code object of "
+                          f"{obj} ({r.stderr.strip()[:200]})")
+            return []
         r = subprocess.run([OBJDUMP, "-d", "--mcpu=gfx950", os.path.join(td, dev[0])], capture_output=True, text=True)
     return [m.group(0).split("//")[0].strip() for m in _PK_OPSEL.finditer(r.stdout) if "1" in m.group(1)]
 

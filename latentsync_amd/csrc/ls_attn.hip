@@ -719,12 +719,7 @@ static int launch_attn5(const AttnArgs& a, int batch, int heads, hipStream_t s) 
   if (nblk > 0x7fffffff) return fail(LS_ERR_INVALID, "ls_attention: grid too large");
   const size_t shm = (3 * (size_t)(KC * 4 + ND * 2) + 1) * 64 * 8 * sizeof(u16);
   if (shm > 64 * 1024) {
-    static bool attr_set = false;
-    if (!attr_set) {
-      hipFuncSetAttribute((const void*)attn5_kernel<KC, ND, DSUM, QG>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)shm);
-      attr_set = true;
-    }
+    LS_SET_MAX_DYN_SHM((attn5_kernel<KC, ND, DSUM, QG>), (int)shm);
   }
   attn5_kernel<KC, ND, DSUM, QG><<<(int)nblk, 256, shm, s>>>(a, nqb, heads);
   return check_launch("attn5_kernel");
@@ -907,9 +902,9 @@ __global__ void __launch_bounds__(NW * 64, 1) attnw_kernel(AttnArgs a, int nqb, 
       for (int f = 0; f < 2; ++f)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = fast_exp2(s[g][f][r]);
-          ps += p;
-          pb[g][4 * f + r] = (__bf16)p;
+          const __bf16 pr = (__bf16)fast_exp2(s[g][f][r]);
+          ps += (float)pr;  // the denominator sums the bf16 P that P.V consumes (as tattn_fused)
+          pb[g][4 * f + r] = pr;
         }
       l[g] += ps;
     }
@@ -962,12 +957,7 @@ static int launch_attnw(const AttnArgs& a, int batch, int heads, hipStream_t s) 
   const long nblk = (long)nqb * heads * batch;
   if (nblk > 0x7fffffff) return fail(LS_ERR_INVALID, "ls_attention: grid too large");
   const size_t shm = (size_t)2 * 2 * (D / 8) * 32 * 8 * sizeof(u16);  // two stages of K + V tiles
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)attnw_kernel<D, QG, NW, PF, SB>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)shm);
-    attr_set = true;
-  }
+  LS_SET_MAX_DYN_SHM((attnw_kernel<D, QG, NW, PF, SB>), (int)shm);
   attnw_kernel<D, QG, NW, PF, SB><<<(int)nblk, NW * 64, shm, s>>>(a, nqb, heads);
   return check_launch("attnw_kernel");
 }
@@ -991,12 +981,7 @@ static int launch_attn3_(const AttnArgs& a, int batch, int heads, hipStream_t s)
   const dim3 grid(cdiv(a.nq, 128), heads, batch);
   const size_t shm = (ONE ? 1 : 2) * 2 * (size_t)64 * (KC * 32 + 8) * sizeof(u16);
   if (shm > 64 * 1024) {
-    static bool attr_set = false;
-    if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)attn3_kernel<KC, ND, DSUM, ONE>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-      attr_set = true;
-    }
+    LS_SET_MAX_DYN_SHM((attn3_kernel<KC, ND, DSUM, ONE>), (int)shm);
   }
   attn3_kernel<KC, ND, DSUM, ONE><<<grid, 256, shm, s>>>(a);
   return check_launch("attn3_kernel");
@@ -1017,11 +1002,7 @@ static int launch_attn(const AttnArgs& a, int batch, int heads, hipStream_t s) {
   const dim3 grid(cdiv(nwant, nw), heads, batch);
   const size_t shm = 2 * (size_t)(16 * NKF) * (DP + 8) * sizeof(u16);
   if (shm > 64 * 1024) {
-    static bool attr_set = false;
-    if (!attr_set) {
-      hipFuncSetAttribute((const void*)attn_kernel<DP, NKF>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-      attr_set = true;
-    }
+    LS_SET_MAX_DYN_SHM((attn_kernel<DP, NKF>), (int)shm);
   }
   attn_kernel<DP, NKF><<<grid, nw * 64, shm, s>>>(a);
   return check_launch("attn_kernel");
@@ -1256,12 +1237,7 @@ template <int D, int HS = 1>
 static int launch_seqm(const AttnArgs& a, int batch, int heads, hipStream_t s) {
   const size_t shm = (size_t)2 * 16 * (heads / HS * D + 8) * sizeof(u16);
   if (shm > 64 * 1024) {
-    static bool attr_set = false;
-    if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)attn_seqm_kernel<D, HS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)shm);
-      attr_set = true;
-    }
+    LS_SET_MAX_DYN_SHM((attn_seqm_kernel<D, HS>), (int)shm);
   }
   attn_seqm_kernel<D, HS><<<dim3(batch, HS), 256, shm, s>>>(a, heads, batch);
   return check_launch("attn_seqm_kernel");
@@ -1272,12 +1248,7 @@ static int launch_seq(const AttnArgs& a, int batch, int heads, hipStream_t s) {
   const int nb = NT / (heads * 16 * TS);
   const int C = heads * D;
   const size_t shm = (size_t)nb * 16 * C * 2 * sizeof(u16);
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)attn_seq_kernel<D, TS, NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)shm);
-    attr_set = true;
-  }
+  LS_SET_MAX_DYN_SHM((attn_seq_kernel<D, TS, NT>), (int)shm);
   attn_seq_kernel<D, TS, NT><<<cdiv(batch, nb), NT, shm, s>>>(a, heads, batch);
   return check_launch("attn_seq_kernel");
 }
@@ -1654,12 +1625,7 @@ static int launch_attn8(const AttnArgs& a, int batch, int heads, uint8_t* ws, hi
   if (nblk > 0x7fffffff) return fail(LS_ERR_INVALID, "ls_attention_fp8: grid too large");
   constexpr int STAGE = 2 * T::KC * 4 * 64 * 8 * 2 + T::TB;
   const size_t shm = (size_t)NST * STAGE + 1024;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)attn8_kernel<D, QG, NST, SB, OCC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)shm);
-    attr_set = true;
-  }
+  LS_SET_MAX_DYN_SHM((attn8_kernel<D, QG, NST, SB, OCC>), (int)shm);
   attn8_kernel<D, QG, NST, SB, OCC><<<(int)nblk, 256, shm, s>>>(a, ws, pb, nqb, heads);
   return check_launch("attn8_kernel");
 }

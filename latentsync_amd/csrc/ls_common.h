@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <atomic>
 #include <string>
 
 #include "../../include/ls_hip.h"
@@ -143,3 +144,19 @@ __device__ __forceinline__ void load8f(const float* __restrict__ p, float* d) {
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 }  // namespace ls
+
+// hipFuncSetAttribute is a per-device setting: apply it once per (call site, device) --
+// a process-wide `static bool` would skip every device after the first one it ran on.
+inline void ls_set_max_dyn_shm(const void* fn, int shm, std::atomic<unsigned long long>& done) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const unsigned long long bit = 1ull << (dev & 63);
+  if (done.load(std::memory_order_acquire) & bit) return;
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, shm);
+  done.fetch_or(bit, std::memory_order_acq_rel);
+}
+#define LS_SET_MAX_DYN_SHM(fn, shm)                                  \
+  do {                                                               \
+    static std::atomic<unsigned long long> ls_shm_done_{0};          \
+    ls_set_max_dyn_shm((const void*)(fn), (int)(shm), ls_shm_done_); \
+  } while (0)

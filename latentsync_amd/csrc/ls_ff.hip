@@ -201,11 +201,7 @@ extern "C" int ls_feedforward(const ls_ff_desc* d, void* stream) {
   a.w2 = (const u16*)d->w2; a.b2 = d->b2; a.y = (u16*)d->y; a.M = d->M; a.ldx = d->ldx; a.ldy = d->ldy;
   constexpr int C = 320, I = 1280;
   const size_t shm = (size_t)2 * (64 * (C / 64) * 8 + C * 4) * 16 + 2 * I * sizeof(float);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)ff_fused_kernel<C, I>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    attr = true;
-  }
+  LS_SET_MAX_DYN_SHM((ff_fused_kernel<C, I>), (int)shm);
   ff_fused_kernel<C, I><<<(unsigned)((d->M + 127) / 128), 512, shm, (hipStream_t)stream>>>(a);
   return check_launch("ff_fused_kernel");
 }

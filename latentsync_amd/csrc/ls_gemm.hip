@@ -1902,12 +1902,7 @@ static void launch_rowblock2(const ConvArgs& a, int grid, hipStream_t s) {
   constexpr int BM = 8 * 16 * FM;
   const size_t shm = (size_t)3 * (16 * FN * (KT / 2) * 8 + 48 + ((FLAGS & RB_RES) ? BM * 16 * FN / 8 : 0)) * 16 +
                      ((FLAGS & RB_GNCS) ? 4096 : 0);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_rowblock_kernel<KT, FM, FN, FLAGS>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    attr = true;
-  }
+  LS_SET_MAX_DYN_SHM((gemm_rowblock_kernel<KT, FM, FN, FLAGS>), (int)shm);
   gemm_rowblock_kernel<KT, FM, FN, FLAGS><<<grid, 512, shm, s>>>(a);
 }
 
@@ -1982,12 +1977,7 @@ template <int BM, int BN, int WM, int WN, int KS, bool TAPU, int NST, int BK, in
 static void launch_dma1(const ConvArgs& a, int grid, hipStream_t s) {
   // staging for the epilogue must fit too
   const size_t shm = std::max<size_t>((size_t)NST * (BM + BN) * (BK / 8) * 16, (size_t)(BM / WM) * (BN + 4) * 4);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_gemm_dma_kernel<BM, BN, WM, WN, KS, TAPU, NST, BK, EPI, BUF>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    attr = true;
-  }
+  LS_SET_MAX_DYN_SHM((conv_gemm_dma_kernel<BM, BN, WM, WN, KS, TAPU, NST, BK, EPI, BUF>), (int)shm);
   conv_gemm_dma_kernel<BM, BN, WM, WN, KS, TAPU, NST, BK, EPI, BUF><<<grid, WM * WN * 64, shm, s>>>(a);
 }
 
@@ -2030,12 +2020,7 @@ static void launch_dma(const ConvArgs& a, int grid, hipStream_t s) {
 template <int BN, int KS, bool TAPU, int EPI, bool BUF = false>
 static void launch_big2(const ConvArgs& a, int grid, hipStream_t s) {
   const size_t shm = std::max<size_t>((size_t)2 * (256 + BN) * 8 * 16, (size_t)128 * (BN + 4) * 4);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_gemm_big_kernel<BN, KS, TAPU, EPI, BUF>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    attr = true;
-  }
+  LS_SET_MAX_DYN_SHM((conv_gemm_big_kernel<BN, KS, TAPU, EPI, BUF>), (int)shm);
   conv_gemm_big_kernel<BN, KS, TAPU, EPI, BUF><<<grid, 512, shm, s>>>(a);
 }
 
@@ -2060,24 +2045,14 @@ static void launch_big1(const ConvArgs& a, int grid, hipStream_t s) {
 template <int KS, bool TAPU>
 static void launch_big4(const ConvArgs& a, int grid, hipStream_t s) {
   const size_t shm = std::max<size_t>((size_t)4 * (256 + 256) * 4 * 16, (size_t)128 * (256 + 4) * 4);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_gemm_big4_kernel<KS, TAPU>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)shm);
-    attr = true;
-  }
+  LS_SET_MAX_DYN_SHM((conv_gemm_big4_kernel<KS, TAPU>), (int)shm);
   conv_gemm_big4_kernel<KS, TAPU><<<grid, 512, shm, s>>>(a);
 }
 
 template <int KS, bool TAPU>
 static void launch_p8_1(const ConvArgs& a, int grid, hipStream_t s) {
   const size_t shm = std::max<size_t>((size_t)2 * 4 * 128 * 8 * 16, (size_t)128 * (256 + 4) * 4);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_gemm_p8_kernel<KS, TAPU>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)shm);
-    attr = true;
-  }
+  LS_SET_MAX_DYN_SHM((conv_gemm_p8_kernel<KS, TAPU>), (int)shm);
   conv_gemm_p8_kernel<KS, TAPU><<<grid, 512, shm, s>>>(a);
 }
 

@@ -320,11 +320,7 @@ template <int C>
 static int launch_tattn(const TAttnArgs& a, int grid, hipStream_t s) {
   using T = TCfg<C>;
   const size_t shm = ((size_t)T::NST * T::STAGE + 64) * 16;  // ring + the dummy DMA slot
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)tattn_fused_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    attr = true;
-  }
+  LS_SET_MAX_DYN_SHM((tattn_fused_kernel<C>), (int)shm);
   tattn_fused_kernel<C><<<grid, T::NT, shm, s>>>(a);
   return check_launch("tattn_fused_kernel");
 }

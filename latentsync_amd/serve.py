@@ -154,26 +154,76 @@ def _worker_main(rank, factory, job_kw, conn):
             conn.send(("err", f"{type(e).__name__}: {e}"))
 
 
+class WorkerDied(RuntimeError):
+    """The GPU worker process ended (fault, abort, OOM kill) or missed the request
+    timeout while serving a request; it has been replaced by a fresh process."""
+
+
 class ProcessWorker:
     """One pipeline process per GPU (spawned, so HIP initialises only in the child).
-    `factory` = "module:function" building the pipeline for a device index."""
+    `factory` = "module:function" building the pipeline for a device index.
 
-    def __init__(self, rank, factory, **job_kw):
+    Robustness (the reference runs the pipeline in-process, api.py:95-190, so a GPU
+    fault kills the whole server): a request that does not finish within
+    `request_timeout` seconds, or whose worker dies under it, fails with WorkerDied
+    and the worker is replaced by a freshly SPAWNED child (never a re-exec of a
+    process that touched the GPU), so the next request routed here is served."""
+
+    def __init__(self, rank, factory, request_timeout=1800.0, start_timeout=900.0, **job_kw):
         self.rank, self.factory, self.job_kw = rank, factory, job_kw
+        self.request_timeout, self.start_timeout = request_timeout, start_timeout
         self.proc = self.conn = None
+        self.restarts = 0
 
-    def start(self):
+    def launch(self):
+        """Spawn the child; `wait_ready` collects its 'ready' (so N GPUs load together)."""
         ctx = mp.get_context("spawn")
         self.conn, child = ctx.Pipe()
         self.proc = ctx.Process(target=_worker_main, args=(self.rank, self.factory, self.job_kw, child), daemon=True)
         self.proc.start()
-        kind, _ = self.conn.recv()
+        child.close()  # the parent keeps one end only: EOF is seen when the child dies
+
+    def wait_ready(self):
+        try:
+            if not self.conn.poll(self.start_timeout):
+                self._kill()
+                raise RuntimeError(f"GPU worker {self.rank} failed to start within {self.start_timeout} s")
+            kind, _ = self.conn.recv()
+        except (EOFError, OSError):
+            self.proc.join(timeout=5)
+            raise RuntimeError(f"GPU worker {self.rank} failed to start (exit code {self.proc.exitcode})") from None
         if kind != "ready":
             raise RuntimeError(f"GPU worker {self.rank} failed to start")
 
+    def start(self):
+        self.launch()
+        self.wait_ready()
+
+    def _kill(self):
+        if self.proc is not None and self.proc.is_alive():
+            self.proc.kill()
+        if self.proc is not None:
+            self.proc.join(timeout=10)
+        if self.conn is not None:
+            self.conn.close()
+
+    def _replace(self):
+        self._kill()
+        self.restarts += 1
+        self.start()
+
     def _call(self, payload):
-        self.conn.send(payload)
-        return self.conn.recv()
+        try:
+            self.conn.send(payload)
+            if not self.conn.poll(self.request_timeout):
+                why = f"timed out after {self.request_timeout} s"
+            else:
+                return self.conn.recv()
+        except (EOFError, OSError):  # BrokenPipeError is an OSError
+            self.proc.join(timeout=5)
+            why = f"died (exit code {self.proc.exitcode})"
+        self._replace()
+        return "dead", f"GPU worker {self.rank} {why} while serving request {payload.get('id')!r}; replaced"
 
     async def run(self, payload):
         loop = asyncio.get_running_loop()
@@ -182,14 +232,20 @@ class ProcessWorker:
             return val
         if kind == "http":
             raise HTTPException(status_code=val[0], detail=val[1])
+        if kind == "dead":
+            raise WorkerDied(val)
         raise RuntimeError(val)
 
     def stop(self):
         if self.proc is not None and self.proc.is_alive():
-            self.conn.send(None)
+            try:
+                self.conn.send(None)
+            except OSError:
+                pass
             self.proc.join(timeout=30)
             if self.proc.is_alive():
                 self.proc.terminate()
+                self.proc.join(timeout=10)
 
 
 # --------------------------------------------------------------------------
@@ -208,8 +264,14 @@ class Dispatcher:
 
     async def start(self):
         self.queue = asyncio.Queue(maxsize=self.queue_size)
+        # every GPU's pipeline loads at once: spawn all children, then wait for their
+        # 'ready' messages together, off the event loop
         for w in self.workers:
-            w.start()
+            (w.launch if hasattr(w, "launch") else w.start)()
+        loop = asyncio.get_running_loop()
+        await asyncio.gather(*[loop.run_in_executor(None, w.wait_ready) for w in self.workers
+                               if hasattr(w, "wait_ready")])
+        for w in self.workers:
             self.tasks.append(asyncio.create_task(self._consume(w)))
 
     async def _consume(self, worker):
@@ -306,9 +368,11 @@ def main():
     ap.add_argument("--factory", default="latentsync_amd.serve:default_pipeline")
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=8000)
+    ap.add_argument("--request-timeout", type=float, default=1800.0,
+                    help="seconds before a request's GPU worker is declared hung and replaced")
     a = ap.parse_args()
     kw = dict(data_dir=a.data_dir, results_dir=a.results_dir, resolution=a.resolution)
-    app = create_app([ProcessWorker(r, a.factory, **kw) for r in range(a.gpus)])
+    app = create_app([ProcessWorker(r, a.factory, request_timeout=a.request_timeout, **kw) for r in range(a.gpus)])
     uvicorn.run(app, host=a.host, port=a.port)
 
 

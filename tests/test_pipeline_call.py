@@ -130,11 +130,24 @@ def test_call_data_pth_with_restore(tmp_path, monkeypatch):
     assert np.load(out_path)["frames"].shape == (n, Rr, Rr, 3)
 
 
-@pytest.mark.parametrize("kw", [dict(use_darken=True), dict(brightness_factor=1.2), dict(weight_dtype=torch.float32)])
+@pytest.mark.parametrize("kw", [dict(use_darken=True), dict(use_darken=True, brightness_factor=1.25),
+                                dict(weight_dtype=torch.float32)])
 def test_call_refuses_unsupported_options(kw):
     """Options whose effect this build does not reproduce raise instead of being
-    ignored: the writer's brightness restore (lipsync_pipeline.py:384-385, :594) and a
+    ignored: the writer's brightness restore, which the reference runs only when
+    `use_darken and brightness_factor` (util.py:150-151, lipsync_pipeline.py:594), and a
     non-half weight_dtype (:374; this path computes in bf16)."""
     pipe = LipsyncPipeline.__new__(LipsyncPipeline)
     with pytest.raises(NotImplementedError):
         pipe(video_path="v.npy", audio_path="a.wav", video_out_path="o.npz", data_path="d.pth", **kw)
+
+
+@pytest.mark.parametrize("kw", [dict(brightness_factor=1.25), dict(brightness_factor=0.8, use_darken=False),
+                                dict(use_darken=True, brightness_factor=0)])
+def test_call_ignores_brightness_without_darken(kw, tmp_path):
+    """The reference ignores brightness_factor unless use_darken is set (and a falsy
+    factor even then): such calls pass the option checks (and here fail only on the
+    absent data file)."""
+    pipe = LipsyncPipeline.__new__(LipsyncPipeline)
+    with pytest.raises(FileNotFoundError):
+        pipe(video_path="v.npy", audio_path="a.wav", video_out_path="o.npz", data_path=str(tmp_path / "d.pth"), **kw)

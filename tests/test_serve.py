@@ -190,3 +190,77 @@ def test_process_worker_spawns_pipeline_process(tmp_path):
     finally:
         w.stop()
     assert not w.proc.is_alive()
+
+
+class _DyingPipeline(StubPipeline):
+    """Ends its process in the middle of the request whose id is 'die' (a GPU fault or
+    an OOM kill as the server sees it), and hangs on 'hang'."""
+
+    def __call__(self, **kw):
+        if kw["video_out_path"].endswith("die.npz"):
+            os._exit(3)
+        if kw["video_out_path"].endswith("hang.npz"):
+            time.sleep(3600)
+        return super().__call__(**kw)
+
+
+def _dying_factory(rank):
+    return _DyingPipeline()
+
+
+def test_process_worker_replaced_after_death_and_timeout(tmp_path):
+    """A worker whose child dies (or misses the request timeout) fails only the request
+    in flight, with WorkerDied, and is replaced by a fresh spawned child that serves
+    the next request (the server is not left routing to a dead GPU process)."""
+    for rid in ("ok1", "die", "ok2", "hang", "ok3"):
+        _files(tmp_path, rid=rid)
+    w = S.ProcessWorker(0, "test_serve:_dying_factory", request_timeout=5.0, data_dir=str(tmp_path),
+                        results_dir=str(tmp_path / "res"))
+    w.start()
+    try:
+        first = w.proc.pid
+        assert asyncio.run(w.run({"id": "ok1", "video_id": "v1", "audio_url": "x"}))["output_url"].endswith("ok1.npz")
+        with pytest.raises(S.WorkerDied, match="died"):
+            asyncio.run(w.run({"id": "die", "video_id": "v1", "audio_url": "x"}))
+        assert w.restarts == 1 and w.proc.pid != first and w.proc.is_alive()
+        assert asyncio.run(w.run({"id": "ok2", "video_id": "v1", "audio_url": "x"}))["output_url"].endswith("ok2.npz")
+        t0 = time.time()
+        with pytest.raises(S.WorkerDied, match="timed out"):
+            asyncio.run(w.run({"id": "hang", "video_id": "v1", "audio_url": "x"}))
+        assert time.time() - t0 < 60 and w.restarts == 2
+        assert asyncio.run(w.run({"id": "ok3", "video_id": "v1", "audio_url": "x"}))["output_url"].endswith("ok3.npz")
+    finally:
+        w.stop()
+    assert not w.proc.is_alive()
+
+
+def _failing_factory(rank):
+    raise SystemExit(7)
+
+
+def test_process_worker_startup_failure_reports_exit_code(tmp_path):
+    w = S.ProcessWorker(0, "test_serve:_failing_factory", data_dir=str(tmp_path), results_dir=str(tmp_path))
+    with pytest.raises(RuntimeError, match="exit code 7"):
+        w.start()
+
+
+def test_brightness_factor_without_darken_is_served(tmp_path):
+    """api.py:136-153 forwards calculate_inverse_factor(brightness_factor) always; the
+    reference pipeline applies it only with use_darken (util.py:150-151).  A request
+    with a recommended factor and use_darken false must reach the pipeline and pass
+    the real LipsyncPipeline's option check."""
+    from latentsync_amd.pipeline import LipsyncPipeline
+    _files(tmp_path)
+    pipe = StubPipeline()
+    _, c = _client(tmp_path, [pipe])
+    with c:
+        r = c.post("/process", json={"id": "r1", "video_id": "v1", "audio_url": "x", "brightness_factor": 0.8,
+                                     "use_darken": False})
+    assert r.status_code == 200
+    kw = pipe.calls[0]
+    assert kw["brightness_factor"] == 1.25 and kw["use_darken"] is False
+    # the real pipeline's guards accept exactly these options: it gets past them and
+    # fails only on the (absent) data file
+    real = LipsyncPipeline.__new__(LipsyncPipeline)
+    with pytest.raises(FileNotFoundError):
+        real(**dict(kw, data_path=str(tmp_path / "absent.pth")))

@@ -1,0 +1,119 @@
+"""A /process request served through a ProcessWorker on cuda:0 by a small REAL
+pipeline (tiny UNet, reduced-width VAE, random-init Whisper-tiny): the spawned worker
+process loads the HIP library, runs LipsyncPipeline.__call__ for the request
+(scripts/api.py:96-190 -> lipsync_pipeline.py:361-604) and writes the frames; the test
+process checks every written window against the CPU oracle's pipeline_window on the
+exact inputs the served pipeline consumed (the worker records them next to its
+output).  The oracle is the checker only: the worker never imports it."""
+import os
+import wave
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+
+SCHED = dict(beta_end=0.012, beta_schedule="scaled_linear", beta_start=0.00085, clip_sample=False,
+             num_train_timesteps=1000, set_alpha_to_one=False, steps_offset=1)
+FR, RR, VAE_CH = 8, 64, (32, 64, 64, 64)
+
+
+def _tiny_pipeline(rank):
+    """ProcessWorker factory (runs in the spawned child, on cuda:rank)."""
+    from latentsync_amd.audio import Audio2Feature
+    from latentsync_amd.config import TINY_MODEL
+    from latentsync_amd.pipeline import LipsyncPipeline
+    from latentsync_amd.scheduler import DDIMScheduler
+    from latentsync_amd.unet import UNet3DConditionModel
+    from latentsync_amd.vae import AutoencoderKL
+
+    class RecordingPipeline(LipsyncPipeline):
+        """Feeds run_windows seeded latents / VAE noise and records its inputs."""
+
+        def __call__(self, **kw):
+            kw["num_frames"] = FR  # the tiny configuration's window
+            kw["num_inference_steps"] = 2
+            self._out = kw["video_out_path"]
+            return super().__call__(**kw)
+
+        def run_windows(self, faces_u8, chunks, mask, num_frames, steps, guidance_scale, generator=None, **kw):
+            n = chunks.shape[0]
+            h = faces_u8.shape[-1] // 8
+            g = torch.Generator().manual_seed(21)
+            init = torch.randn((1, 4, 1, h, h), generator=g).repeat(1, 1, n, 1, 1)
+            nw = -(-n // num_frames)
+            noise = [(torch.randn((min(num_frames, n - i * num_frames), 4, h, h), generator=g),
+                      torch.randn((min(num_frames, n - i * num_frames), 4, h, h), generator=g)) for i in range(nw)]
+            np.savez(self._out.replace(".npz", "_inputs.npz"), faces=faces_u8[:n].cpu().numpy(),
+                     chunks=chunks.float().cpu().numpy(), mask=mask.cpu().numpy(), init=init.numpy(),
+                     em=np.concatenate([a for a, _ in noise]), er=np.concatenate([b for _, b in noise]),
+                     steps=steps, guidance=guidance_scale)
+            return super().run_windows(faces_u8, chunks, mask, num_frames, steps, guidance_scale,
+                                       all_latents=init.to(self.device),
+                                       vae_noise=lambda i: (noise[i][0].to(self.device), noise[i][1].to(self.device)),
+                                       **kw)
+
+    dev = torch.device("cuda", rank)
+    unet = UNet3DConditionModel(**TINY_MODEL).init_weights(3).to(dev).eval()
+    vae = AutoencoderKL(block_out_channels=VAE_CH).init_weights(4).to(dev)
+    return RecordingPipeline(vae, Audio2Feature.random(2, device=dev), unet, DDIMScheduler(**SCHED))
+
+
+def _write_wav(path, seconds, sr=16000):
+    a = np.random.default_rng(1).normal(0, 0.1, int(seconds * sr)).clip(-1, 0.999)
+    with wave.open(str(path), "wb") as f:
+        f.setnchannels(1)
+        f.setsampwidth(2)
+        f.setframerate(sr)
+        f.writeframes((a * 32768).astype("<i2").tobytes())
+
+
+def test_process_request_through_gpu_worker(tmp_path, monkeypatch):
+    from fastapi.testclient import TestClient
+
+    from latentsync_amd import serve as S
+    from oracle import ref_cpu as R
+
+    N = 24
+    g = torch.Generator().manual_seed(5)
+    faces = (torch.rand((N, 3, RR, RR), generator=g) * 255).to(torch.uint8)
+    torch.save({"faces": faces, "boxes": [[0, 0, RR, RR]] * N,
+                "affine_matrices": [np.eye(2, 3)] * N}, tmp_path / "v1.pth")
+    open(tmp_path / "v1.mp4", "wb").close()  # not an array file: the aligned faces are written (no warp-back)
+    _write_wav(tmp_path / "src.wav", 0.7)
+    worker = S.ProcessWorker(0, "test_serve_gpu:_tiny_pipeline", request_timeout=300.0, data_dir=str(tmp_path),
+                             results_dir=str(tmp_path / "res"), resolution=RR)
+    app = S.create_app([worker])
+    with TestClient(app) as c:
+        assert c.get("/ping").json() == {"message": "pong"}
+        r = c.post("/process", json={"id": "req1", "video_id": "v1", "audio_url": "file://" + str(tmp_path / "src.wav"),
+                                     "brightness_factor": 0.8, "use_darken": False})
+        assert r.status_code == 200, r.text
+        body = r.json()
+    assert body["message"] == "Request processed successfully"
+    out = np.load(body["output_url"])["frames"]
+    inp = np.load(body["output_url"].replace(".npz", "_inputs.npz"))
+    n = inp["chunks"].shape[0]
+    assert out.shape == (n, RR, RR, 3) and out.dtype == np.uint8 and n % FR == 0 and n > 0
+    monkeypatch.setitem(R.VAE_CFG, "block_out_channels", VAE_CH)
+    from latentsync_amd.config import TINY_MODEL
+    from latentsync_amd.unet import UNet3DConditionModel
+    from latentsync_amd.vae import AutoencoderKL
+    unet = UNet3DConditionModel(**TINY_MODEL).init_weights(3)  # the worker's weights, on the host
+    vae = AutoencoderKL(block_out_channels=VAE_CH).init_weights(4)
+    em, er, init = torch.from_numpy(inp["em"]), torch.from_numpy(inp["er"]), torch.from_numpy(inp["init"])
+    mask = torch.from_numpy(inp["mask"])
+    for w in range(n // FR):
+        sl = slice(w * FR, (w + 1) * FR)
+        ref = R.pipeline_window(unet.state_dict(), dict(unet.config), vae._sd, torch.from_numpy(inp["faces"][sl]),
+                                mask, torch.from_numpy(inp["chunks"][sl]), init[:, :, sl][:, :, :1], em[sl], er[sl],
+                                num_steps=int(inp["steps"]), guidance_scale=float(inp["guidance"]))
+        ref_u8 = ((ref / 2 + 0.5).clamp(0, 1) * 255).permute(0, 2, 3, 1).numpy()
+        got = out[sl].astype(np.float64)
+        e = rel_err(got / 255.0 * 2 - 1, torch.from_numpy(ref_u8 / 255.0 * 2 - 1))
+        d = np.abs(got - ref_u8)
+        print("served window", w, "rel", e, "max", d.max(), "p99.9", np.percentile(d, 99.9))
+        assert e < 3e-2 and d.max() <= 12 and np.percentile(d, 99.9) <= 6
