@@ -88,7 +88,9 @@ def _worker(rank, world, port, n, q):
         setattr(dist, name, counted)
     try:
         out, out8 = _run(_pipe(), n)
-        q.put((rank, calls, out, out8))
+        # by value (numpy), not torch's fd-shared storage: this process may exit before
+        # the parent unpickles, and the storage's fd listener goes with it
+        q.put((rank, calls, out.numpy(), out8.numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -109,7 +111,7 @@ def test_run_windows_one_collective(world, n):
         assert p.exitcode == 0
     for rank, calls, out, out8 in res:
         assert calls == ["all_gather"], (rank, calls)  # gloo's form of all_gather_into_tensor
-        assert torch.equal(out, ref) and torch.equal(out8, ref8), rank
+        assert torch.equal(torch.from_numpy(out), ref) and torch.equal(torch.from_numpy(out8), ref8), rank
 
 
 def test_frames_to_u8_matches_paste_back_rounding():
