@@ -725,6 +725,263 @@ static int launch_attn5(const AttnArgs& a, int batch, int heads, hipStream_t s) 
   return check_launch("attn5_kernel");
 }
 
+// attn6: the d = 40 self attention (UNet 32x32 level; 64x64 at configs[4]) on
+// v_mfma_f32_32x32x16_bf16.  attn5 is issue-bound, not MFMA-bound: per 64-key tile and
+// wave it issues 64 v_exp_f32 (8 cycles each) beside 56 16x16x32 MFMAs that each hold the
+// SIMD's vector issue for 8 of their 16 cycles (448 cycles), so the ~1350 issue cycles of
+// a tile exceed its 896 MFMA cycles.  The 32x32x16 form holds issue 8 of 32 cycles: the
+// same 896 MFMA cycles (QK^T: 2 query x 2 key tiles x 3 k-steps over d padded to 48;
+// P V: 2 query x 2 d tiles x 4 key steps over d padded to 64, row 40 = the sum column)
+// cost 224 issue cycles instead of 448.
+//   * S^T = K Q^T per (query tile qt, key tile kt): a lane holds query r32 = lane & 31
+//     and 16 keys (i & 3) + 8 (i >> 2) + 4 hh of the tile (hh = lane >> 5), so the row
+//     max is 31 maxima + one permlane32 swap; C = -m (a 16-register splat per qt).
+//   * The accumulator IS the next MFMA's B operand (cdna_hip_programming.md §3, "an
+//     accumulator tile as the next MFMA's operand"): registers 8s .. 8s+7 of S^T are
+//     k-step s of O^T += V^T P^T with element j = key 16s + 8(j>>2) + 4hh + (j&3); the V^T
+//     fragment takes the same key order by two ds_read_b64_tr_b16 (4 keys each).
+//   * V plane c stores key k at position k ^ 4 (c & 3) (attn5 rotates by 8 keys per plane)
+//     so the 32-lane halves of those transposed reads, which span 4 planes, hit 32 distinct
+//     8-B bank slots; the XOR leaves bit 5 alone, so the second 32-key half of a tile is a
+//     uniform offset.
+// Same DMA ring, lazy rescale and XCD-aware block order as attn5.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float swap32_max(float v) {
+  const uint32_t u = __float_as_uint(v);
+  const auto a = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __builtin_elementwise_maximum(__uint_as_float(a[0]), __uint_as_float(a[1]));
+}
+
+template <int DSUM>
+__global__ void __launch_bounds__(256, 2) attn6_kernel(AttnArgs a, int nqb, int heads) {
+  constexpr int KT = 64;
+  constexpr int NST = 3;
+  constexpr int KPL = 6;        // K planes: d 0..47 (3 k-steps of 16)
+  constexpr int VPL = 8;        // V planes: d 0..63 (two 32-row O^T tiles)
+  constexpr int PLANE = KT * 8;
+  constexpr int STAGE = (KPL + VPL) * PLANE;
+  constexpr float TAU = 10.f;
+  static_assert(DSUM == 40, "attn6 is the d = 40 kernel (sum column at d = 40)");
+  extern __shared__ __attribute__((aligned(16))) u16 sm[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lb = attn_xcd_remap(blockIdx.x, gridDim.x);
+  const int qblk = lb % nqb, pair = lb / nqb;
+  const int h = pair % heads;
+  const int b = pair / heads;
+  const long b1 = b / a.z2, b2 = b - b1 * a.z2;
+  const u16* qb = a.q + b1 * a.q_sb1 + b2 * a.q_sb2 + (long)h * a.q_sh;
+  const u16* kb = a.k + b1 * a.k_sb1 + b2 * a.k_sb2 + (long)h * a.k_sh;
+  const u16* vb = a.v + b1 * a.v_sb1 + b2 * a.v_sb2 + (long)h * a.v_sh;
+  u16* ob = a.o + b1 * a.o_sb1 + b2 * a.o_sb2 + (long)h * a.o_sh;
+  const int q0 = (qblk * 4 + wid) * 64;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int cpr = (a.D + 7) >> 3;  // planes that carry data (5)
+
+  // constant planes of every stage: K's zero, V's sum column / zero (a constant plane
+  // reads the same under any key rotation)
+  for (int i = tid; i < NST * (KPL + VPL) * KT; i += 256) {
+    const int r = i % KT, c = (i / KT) % (KPL + VPL), st = i / (KT * (KPL + VPL));
+    const bool isv = c >= KPL;
+    const int cc = isv ? c - KPL : c;
+    if (cc >= cpr)
+      *(uint4*)(sm + st * STAGE + c * PLANE + r * 8) = make_uint4(isv && cc * 8 == DSUM ? 0x3F80u : 0u, 0, 0, 0);
+  }
+
+  // Q^T fragments (B operand): lane (r32, hh) holds Q[q0 + 32 qt + r32][16 ks + 8 hh .. + 8]
+  const float c2 = a.scale_log2;
+  bf16x8 qf[2][3];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) {
+      const int d = ks * 16 + hh * 8;
+      const int q = q0 + qt * 32 + r32;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (q < a.nq && d < a.D) v = *(const uint4*)(qb + (long)q * a.q_si + d);
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] *= c2;
+      qf[qt][ks] = __builtin_bit_cast(bf16x8, pack8(f));
+    }
+
+  const uint32_t kst = (uint32_t)a.k_si * 2, vst = (uint32_t)a.v_si * 2;
+  const i32x4 krs = buffer_rsrc(kb, (uint32_t)(a.nk - 1) * kst + cpr * 16);
+  const i32x4 vrs = buffer_rsrc(vb, (uint32_t)(a.nk - 1) * vst + cpr * 16);
+  constexpr int NDMA = 3;  // ceil(2 * 5 planes / 4 waves); extra loads go to the dummy plane
+  u16* dummy = sm + NST * STAGE;
+  auto issue = [&](int t) {
+    const int t0 = t * KT;
+    u16* st = sm + (t % NST) * STAGE;
+#pragma unroll
+    for (int u = 0; u < NDMA; ++u) {
+      const int j = wid + 4 * u;  // wave-uniform
+      const bool live = j < 2 * cpr;
+      const bool isv = live && j >= cpr;
+      const int c = !live ? 0 : (isv ? j - cpr : j);
+      const int key = isv ? (lane ^ (4 * (c & 3))) : lane;  // V: position p holds key p ^ 4 (c & 3)
+      u16* dst = live ? st + ((isv ? KPL : 0) + c) * PLANE : dummy;
+      ls_raw_buffer_load_lds(isv ? vrs : krs, (__attribute__((address_space(3))) void*)dst, 16,
+                             key * (int)(isv ? vst : kst) + c * 16, t0 * (int)(isv ? vst : kst), 0, 0);
+    }
+  };
+
+  f32x16 oacc[2][2];
+  f32x16 negm[2];
+  float m[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    m[qt] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      oacc[qt][0][i] = 0.f;
+      oacc[qt][1][i] = 0.f;
+      negm[qt][i] = 0.f;
+    }
+  }
+
+  // per-lane LDS element offsets of the V^T fragment reads (tile-invariant): group
+  // g = lane >> 4 reads keys 4 (g >> 1) + q, d = 32 dt + 16 (g & 1) + 4 p (lane 4q + p)
+  const int gi = lane & 15, tq = gi >> 2, tp = gi & 3, gg = lane >> 4;
+  int voff[2][2][2];  // [dt][s][half of the key step]
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    const int pl = 4 * dt + 2 * (gg & 1) + (tp >> 1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int key = 16 * s + 8 * e + 4 * (gg >> 1) + tq;  // within a 32-key tile (+ 32 kt below)
+        voff[dt][s][e] = pl * PLANE + (key ^ (4 * (pl & 3))) * 8 + (tp & 1) * 4;
+      }
+  }
+
+  const int ntile = (a.nk + KT - 1) / KT;
+  issue(0);
+  if (ntile > 1) issue(1);
+  auto tile = [&](int t, auto partial_tag) {
+    constexpr bool PARTIAL = decltype(partial_tag)::value;
+    const int t0 = t * KT;
+    if (t + 1 < ntile) attn_wait_vm<NDMA>();
+    else attn_wait_vm<0>();
+    __syncthreads();
+    if (t + 2 < ntile) issue(t + 2);
+    const u16* Ks = sm + (t % NST) * STAGE;
+    const u16* Vs = Ks + KPL * PLANE;
+    f32x16 s[2][2];  // [qt][kt]
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        const bf16x8 kf =
+            __builtin_bit_cast(bf16x8, *(const uint4*)(Ks + (2 * ks + hh) * PLANE + (32 * kt + r32) * 8));
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+          s[qt][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[qt][ks], ks == 0 ? negm[qt] : s[qt][kt], 0, 0, 0);
+      }
+    }
+    float mt[2];
+    bool need_any = t == 0;
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      if (PARTIAL) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (t0 + 32 * kt + (i & 3) + 8 * (i >> 2) + 4 * hh >= a.nk) s[qt][kt][i] = -INFINITY;
+      }
+      float x = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; i += 2)
+          x = __builtin_elementwise_maximum(x, __builtin_elementwise_maximum(s[qt][kt][i], s[qt][kt][i + 1]));
+      mt[qt] = swap32_max(x);
+      need_any |= mt[qt] > TAU;
+    }
+    if (__builtin_amdgcn_ballot_w64(need_any)) {
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        const bool need = t == 0 || mt[qt] > TAU;
+        const float dlt = need ? mt[qt] : 0.f;
+        const float alpha = t == 0 ? 0.f : fast_exp2(-dlt);
+        m[qt] += dlt;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) negm[qt][i] = -m[qt];
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) s[qt][kt] -= dlt;
+        oacc[qt][0] *= alpha;
+        oacc[qt][1] *= alpha;
+      }
+    }
+    // P = exp2(S^T - m), then O^T += V^T P^T over 4 key steps of 16
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[qt][kt][i] = fast_exp2(s[qt][kt][i]);
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        bf16x8 pb[2];
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pb[qt][j] = (__bf16)s[qt][kt][8 * st + j];
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const u16* vk = Vs + 32 * kt * 8;  // key 32 kt of every plane (the XOR keeps bit 5)
+          const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) v4i16*)(vk + voff[dt][st][0]));
+          const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) v4i16*)(vk + voff[dt][st][1]));
+          const short __attribute__((ext_vector_type(8))) av = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          const bf16x8 vf = __builtin_bit_cast(bf16x8, av);
+#pragma unroll
+          for (int qt = 0; qt < 2; ++qt)
+            oacc[qt][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb[qt], oacc[qt][dt], 0, 0, 0);
+        }
+      }
+    }
+  };
+  const int nfull = a.nk / KT;
+  for (int t = 0; t < nfull; ++t) tile(t, std::false_type{});
+  if (nfull < ntile) tile(nfull, std::true_type{});
+  // l = O^T row 40: d tile 1, row 8 -> register 4 of the half hh = 0
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const float lt = __shfl(oacc[qt][1][4], r32, 64);
+    const float inv = 1.f / lt;
+    const int q = q0 + qt * 32 + r32;
+    if (q < a.nq) {
+      u16* orow = ob + (long)q * a.o_si;
+#pragma unroll
+      for (int g = 0; g < 5; ++g) {  // d = 8 g' + 4 hh .. +3: dt 0 rows 4g..4g+3 (g < 4), dt 1 rows 0..3
+        const int dt = g >> 2, rg = g & 3;
+        const int d = 32 * dt + 8 * rg + 4 * hh;
+        uint2 w;
+        w.x = pack2(oacc[qt][dt][4 * rg] * inv, oacc[qt][dt][4 * rg + 1] * inv);
+        w.y = pack2(oacc[qt][dt][4 * rg + 2] * inv, oacc[qt][dt][4 * rg + 3] * inv);
+        *(uint2*)(orow + d) = w;
+      }
+    }
+  }
+}
+
+template <int DSUM>
+static int launch_attn6(const AttnArgs& a, int batch, int heads, hipStream_t s) {
+  const int nqb = cdiv(a.nq, 4 * 64);
+  const long nblk = (long)nqb * heads * batch;
+  if (nblk > 0x7fffffff) return fail(LS_ERR_INVALID, "ls_attention: grid too large");
+  const size_t shm = (3 * (size_t)(6 + 8) + 1) * 64 * 8 * sizeof(u16);
+  LS_SET_MAX_DYN_SHM((attn6_kernel<DSUM>), (int)shm);
+  attn6_kernel<DSUM><<<(int)nblk, 256, shm, s>>>(a, nqb, heads);
+  return check_launch("attn6_kernel");
+}
+
 // attnw: wide heads -- the SD-VAE mid-block attention (1 head, d = 512, N = h w tokens;
 // diffusers Attention).  Replaces attn_kernel<512,4> (0.068 of the
 // dense peak: K / V staged synchronously behind two barriers per tile, no prefetch, one
@@ -1636,6 +1893,7 @@ using namespace ls;
 
 static bool g_attn_v1 = getenv("LS_ATTN_V1") != nullptr;  // A/B switch: force the 16-query kernel
 static bool g_attn_v3 = getenv("LS_ATTN_V3") != nullptr;  // A/B switch: attn3 for d = 40 too
+static bool g_attn5 = getenv("LS_ATTN5") != nullptr;  // A/B switch: d = 40 self attention on attn5 (16x16x32)
 static bool g_attnw_off = getenv("LS_ATTNW_OFF") != nullptr;  // A/B switch: d = 512 on attn_kernel
 static bool g_seq_valu = getenv("LS_ATTN_SEQ_VALU") != nullptr;  // A/B switch: dot-product short-sequence kernel
 static bool g_seq160_valu = getenv("LS_ATTN_SEQ160_VALU") != nullptr;  // A/B switch: ... for d = 160 only
@@ -1736,7 +1994,7 @@ extern "C" int ls_attention(const ls_attn_desc* d, void* stream) {
     // queries per wave, row sums from the PV MFMA; short key sets (the 50 audio tokens)
     // and other head dims: attn3 (register-staged tiles)
     if (D == 40 && !g_attn_v3 && d->nk > 128 && ((long)(d->nk - 1) * std::max(d->k_si, d->v_si) + D) * 2 < (1L << 31))
-      return launch_attn5<2, 3, 40, 4>(a, d->batch, d->heads, s);
+      return g_attn5 ? launch_attn5<2, 3, 40, 4>(a, d->batch, d->heads, s) : launch_attn6<40>(a, d->batch, d->heads, s);
     if (D == 40) return launch_attn3<2, 3, 40>(a, d->batch, d->heads, s);
     switch ((D + 15) / 16) {
       case 1: case 2: return launch_attn3<1, 2, 0>(a, d->batch, d->heads, s);

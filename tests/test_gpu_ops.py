@@ -191,6 +191,32 @@ def test_attention_d512_rescale(gpu, qscale):
     assert rel_err(o.float().cpu(), ref) < 1.5e-2
 
 
+@pytest.mark.parametrize("qscale,N,Nk", [(1.0, 1024, 1024), (3.0, 1024, 1024), (3.0, 777, 1000)])
+def test_attention_d40_rescale_fused_qkv(gpu, qscale, N, Nk):
+    """The d = 40 self-attention kernel (attn6, 32x32x16 MFMA) on the UNet's fused q|k|v
+    rows (row stride 3C) with keys whose scores grow along the sequence, so the running
+    max moves past the lazy-rescale threshold on later tiles (qscale 3: log2-unit logits
+    past 20); ragged query / key counts in the last case."""
+    n, heads, d = 2, 8, 40
+    C = heads * d
+    q = rnd(n, N, C, seed=70) * qscale
+    k = rnd(n, Nk, C, seed=71) * torch.linspace(0.2, 2.0, Nk).reshape(1, Nk, 1)
+    v = rnd(n, Nk, C, seed=72)
+    q, k, v = bf(q), bf(k), bf(v)
+    split = lambda t: t.reshape(t.shape[0], t.shape[1], heads, d).permute(0, 2, 1, 3)
+    ref = _sdpa(split(q), split(k), split(v)).permute(0, 2, 1, 3).reshape(n, N, C)
+    L = max(N, Nk)
+    qkv = torch.zeros((n, L, 3 * C), dtype=torch.bfloat16)
+    qkv[:, :N, :C], qkv[:, :Nk, C:2 * C], qkv[:, :Nk, 2 * C:] = q.to(torch.bfloat16), k.to(torch.bfloat16), \
+        v.to(torch.bfloat16)
+    qkv = qkv.to(DEV).reshape(n * L, 3 * C)
+    o = torch.empty((n * N, C), dtype=torch.bfloat16, device=DEV)
+    st = (L * 3 * C, 0, 3 * C, d)
+    ops.attention(qkv, qkv[:, C:], qkv[:, 2 * C:], o, batch=n, z2=1, heads=heads, nq=N, nk=Nk, head_dim=d, qs=st,
+                  ks=st, vs=st, os_=(N * C, 0, C, d))
+    assert rel_err(o.float().cpu().reshape(n, N, C), ref) < 1.5e-2
+
+
 @pytest.mark.parametrize("C,Fr,S", [(320, 16, 16), (640, 16, 16), (1280, 16, 16), (320, 12, 15), (640, 7, 9),
                                     (1280, 16, 3)])
 def test_attention_temporal_strided(gpu, C, Fr, S):
