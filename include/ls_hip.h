@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LS_ABI_VERSION 11
+#define LS_ABI_VERSION 12
 
 typedef enum {
   LS_OK = 0,
@@ -271,6 +271,37 @@ typedef struct {
 } ls_ff_desc;
 
 int ls_feedforward(const ls_ff_desc* d, void* stream);
+
+/*
+ * The audio cross-attention branch of a BasicTransformerBlock, one launch (ABI 12;
+ * attention.py:174-199 norm2 + attn2, Attention.forward :250-280 with the Whisper chunks
+ * as encoder_hidden_states; replaces the LN-folded to_q GEMM + ls_attention + the
+ * to_out GEMM with its residual):
+ *   y = x + Wo softmax((Wq LN(x) + bq) K^T / sqrt(d)) V + bo
+ * and stats_out = (mean, rstd) of the stored y rows (eps; norm3's LayerNorm fold).
+ * x, y: bf16 rows [M][ldx] / [M][ldy], hw rows per image (a multiple of 128, M a multiple
+ * of hw); ln_rowstats: (mean, rstd) of the x rows; kv: bf16 [M / hw * L][ldkv] rows of
+ * to_k | to_v of the image's L audio tokens (L <= 64); wq / bq: packing.pack_xattn_q
+ * (per head 48 rows with LayerNorm gamma / beta and log2(e) / sqrt(d) folded, k-images
+ * swizzled); wo: packing.pack_xattn_wo (columns permuted to the kernel's k-slot order,
+ * padding slots zero); bo: fp32 [C].  C = 320, 8 heads (the 32x32 level) only.
+ */
+typedef struct {
+  const void* x;
+  const float* ln_rowstats;
+  const void* wq;
+  const float* bq;
+  const void* kv;
+  const void* wo;
+  const float* bo;
+  void* y;
+  float* stats_out;
+  int64_t M;
+  int32_t ldx, ldy, ldkv, C, heads, L, hw;
+  float eps;
+} ls_xattn_desc;
+
+int ls_cross_attention_block(const ls_xattn_desc* d, void* stream);
 
 /*
  * Small-M linear in fp32: y[m, n] = sum_k act(x[m, k]) * W[n, k] + bias[n]

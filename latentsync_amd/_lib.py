@@ -10,7 +10,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LS_HIP_LIB", os.path.join(HERE, "libls_hip.so"))
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 c_u16p = C.c_void_p
 c_vp = C.c_void_p
@@ -60,6 +60,13 @@ class FFDesc(C.Structure):
                 ("inner", C.c_int32)]
 
 
+class XAttnDesc(C.Structure):
+    _fields_ = [("x", c_vp), ("ln_rowstats", c_vp), ("wq", c_vp), ("bq", c_vp), ("kv", c_vp), ("wo", c_vp),
+                ("bo", c_vp), ("y", c_vp), ("stats_out", c_vp), ("M", C.c_int64), ("ldx", C.c_int32),
+                ("ldy", C.c_int32), ("ldkv", C.c_int32), ("C", C.c_int32), ("heads", C.c_int32), ("L", C.c_int32),
+                ("hw", C.c_int32), ("eps", C.c_float)]
+
+
 _SIGS = {
     "ls_abi_version": (C.c_int, []),
     "ls_last_error": (C.c_char_p, []),
@@ -82,6 +89,7 @@ _SIGS = {
     "ls_attention_fp8": (C.c_int, [C.POINTER(AttnDesc), c_vp, C.c_size_t, c_vp]),
     "ls_temporal_attention": (C.c_int, [C.POINTER(TAttnDesc), c_vp]),
     "ls_feedforward": (C.c_int, [C.POINTER(FFDesc), c_vp]),
+    "ls_cross_attention_block": (C.c_int, [C.POINTER(XAttnDesc), c_vp]),
     "ls_small_linear": (C.c_int, [c_vp, C.c_int32, C.c_int32, c_vp, c_vp, C.c_int32, C.c_int32, c_vp, c_vp]),
     "ls_timestep_embed": (C.c_int, [c_vp, c_vp, C.c_int32, C.c_int32, C.c_int32, C.c_float, c_vp, c_vp]),
     "ls_ddim_cfg_step": (C.c_int, [c_vp, C.c_int32, C.c_int32, C.c_int64, C.c_float, c_vp, c_vp, c_vp, c_vp,

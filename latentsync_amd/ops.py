@@ -334,6 +334,52 @@ def feedforward(x2d, ln_stats, w1: "Packed", w2: "Packed", w2ff, out=None):
     return out
 
 
+class XAttnPack:
+    """ls_cross_attention_block operands of one BasicTransformerBlock's attn2 + norm2
+    (packing.pack_xattn_q / pack_xattn_wo)."""
+
+    def __init__(self, wq, bq, wo, bo, C, heads):
+        self.wq, self.bq, self.wo, self.bo, self.C, self.heads = wq, bq, wo, bo, C, heads
+
+
+def pack_cross_attention(wq, ln_weight, ln_bias, wo, bo, heads, device):
+    """XAttnPack from the reference tensors: to_q.weight (C, C), norm2 gamma / beta,
+    to_out.0.weight (C, C) / bias -- LayerNorm folded (W gamma, W beta) in fp32 before the
+    single bf16 rounding."""
+    from .packing import pack_xattn_q, pack_xattn_wo
+    w = wq.float().cpu()
+    gamma, beta = ln_weight.float().cpu(), ln_bias.float().cpu()
+    pq, pb = pack_xattn_q(w * gamma[None, :], w @ beta, heads)
+    po = pack_xattn_wo(wo.float().cpu(), heads)
+    bf = lambda t: t.to(torch.bfloat16).to(device).contiguous()
+    return XAttnPack(bf(pq), pb.to(device).contiguous(), bf(po), bo.float().to(device).contiguous(), w.shape[0], heads)
+
+
+def cross_attention_ok(x2d, pk, L, hw):
+    """Shapes ls_cross_attention_block takes (else q GEMM + ls_attention + out GEMM)."""
+    return (pk is not None and x2d.shape[1] == 320 and pk.heads == 8 and 1 <= L <= 64 and hw % 128 == 0
+            and x2d.shape[0] % hw == 0 and x2d.stride(1) == 1 and x2d.stride(0) % 8 == 0)
+
+
+def cross_attention_block(x2d, ln_stats, pk: XAttnPack, kv, L, hw, stats_out, out=None, eps=1e-5):
+    """y = x + to_out(attn(to_q(LN(x)), k, v)) for the audio cross attention in one launch
+    (ls_cross_attention_block); stats_out (M, 2) receives y's LayerNorm row statistics."""
+    lib = _lib.load()
+    M, C_ = x2d.shape
+    if out is None:
+        out = torch.empty((M, C_), dtype=torch.bfloat16, device=x2d.device)
+    assert stats_out.dtype == torch.float32 and stats_out.is_contiguous() and stats_out.numel() == 2 * M
+    assert kv.stride(1) == 1 and kv.shape[0] == (M // hw) * L and kv.shape[1] >= 2 * C_
+    d = _lib.XAttnDesc()
+    d.x, d.ln_rowstats, d.wq, d.bq, d.kv, d.wo, d.bo = _p(x2d), _p(ln_stats), _p(pk.wq), _p(pk.bq), _p(kv), \
+        _p(pk.wo), _p(pk.bo)
+    d.y, d.stats_out = _p(out), _p(stats_out)
+    d.M, d.ldx, d.ldy, d.ldkv, d.C, d.heads, d.L, d.hw, d.eps = M, x2d.stride(0), out.stride(0), kv.stride(0), C_, \
+        pk.heads, L, hw, eps
+    check(lib.ls_cross_attention_block(C.byref(d), _stream()), "ls_cross_attention_block")
+    return out
+
+
 def attention_fp8_workspace_bytes(*, batch, heads, nk, head_dim):
     lib = _lib.load()
     d = _lib.AttnDesc()

@@ -89,3 +89,62 @@ def pack_ff_w2(w2: torch.Tensor) -> torch.Tensor:
     out = torch.empty_like(w)
     out[rows[:, None], :, phys, :] = w.permute(0, 2, 1, 3)       # (C, piece, chunk, 8) scattered
     return out.permute(1, 0, 2, 3).reshape(I // 32, C, 32).contiguous()
+
+
+def _xattn_slot_dims():
+    """Head-local (head offset, dim) of every k-slot of the fused cross-attention's
+    out-projection (ls_cross_attention_block): k-step 3j + u, lane group lg, element e.
+    u = 0, 1: head 2j + u, dims 4 lg + e (e < 4) / 16 + 4 lg + e - 4; u = 2: dims 32 + 4 lg
+    + (e & 3) of head 2j (e < 4) / 2j + 1 (e >= 4), lane groups 2, 3 padding (None)."""
+    out = []
+    for ks in range(12):
+        j, u = divmod(ks, 3)
+        for lg in range(4):
+            for e in range(8):
+                if u < 2:
+                    out.append((2 * j + u, 4 * lg + e if e < 4 else 16 + 4 * lg + e - 4))
+                elif lg < 2:
+                    out.append((2 * j + (e >= 4), 32 + 4 * lg + (e & 3)))
+                else:
+                    out.append(None)
+    return out
+
+
+def pack_xattn_q(wq: torch.Tensor, bq: torch.Tensor, heads: int = 8):
+    """to_q with norm2's gamma / beta folded (the LN-folded operand: W (C, C), bias (C))
+    -> ls_cross_attention_block's wq [heads][C/64 k-images][48 rows][8 pieces][8] bf16 and
+    bq [heads][48] fp32: each head's 40 rows padded to 48 (zero), scaled by log2(e)/sqrt(d)
+    (the kernel's softmax works in log2 units), 16-B pieces of a 64-wide k-image stored at
+    physical piece lc ^ ((row >> 1) & 7) (the row-block GEMM's swizzle)."""
+    import math
+    C = wq.shape[0]
+    d = C // heads
+    sc = math.log2(math.e) / math.sqrt(d)
+    w = torch.zeros(heads, 48, C)
+    w[:, :d] = wq.float().reshape(heads, d, C) * sc
+    b = torch.zeros(heads, 48)
+    b[:, :d] = bq.float().reshape(heads, d) * sc
+    w = w.reshape(heads, 48, C // 64, 8, 8).permute(0, 2, 1, 3, 4)  # (head, img, row, logical piece, 8)
+    rows = torch.arange(48)
+    phys = torch.arange(8)[None, :] ^ ((rows[:, None] >> 1) & 7)    # (row, logical) -> physical
+    out = torch.empty_like(w)
+    out[:, :, rows[:, None], phys, :] = w
+    return out.contiguous(), b.contiguous()
+
+
+def pack_xattn_wo(wo: torch.Tensor, heads: int = 8):
+    """to_out (C, C) -> ls_cross_attention_block's wo [C/32 chunks][2 tiles][12 k-steps][16
+    rows][4 pieces][8] bf16: column slots in the kernel's o register order
+    (_xattn_slot_dims), padding slots zero, the 16-B pieces of a row at physical piece
+    lg ^ (((row >> 3) & 1) << 1) (conflict-free ds_read_b128, as pack_ff_w2)."""
+    C = wo.shape[0]
+    d = C // heads
+    idx = torch.tensor([40 * 0 + 0 if s is None else s[0] * d + s[1] for s in _xattn_slot_dims()])
+    valid = torch.tensor([s is not None for s in _xattn_slot_dims()])
+    w = wo.float()[:, idx] * valid[None, :].float()                  # (C out, 384 slots)
+    w = w.reshape(C // 32, 2, 16, 12, 4, 8).permute(0, 1, 3, 2, 4, 5)  # (chunk, tile, ks, row, lg, 8)
+    rows = torch.arange(16)
+    phys = torch.arange(4)[None, :] ^ (((rows[:, None] >> 3) & 1) << 1)
+    out = torch.empty_like(w)
+    out[:, :, :, rows[:, None], phys, :] = w
+    return out.contiguous()

@@ -37,6 +37,8 @@ from .weights import fill_state_dict
 _FUSED_TEMPORAL = os.environ.get("LS_FUSED_TEMPORAL", "1") != "0"
 # LS_FUSED_FF=0: the FeedForward as GEGLU row-block GEMM + W2 GEMM (A/B switch)
 _FUSED_FF = os.environ.get("LS_FUSED_FF", "1") != "0"
+# LS_FUSED_XATTN=0: the audio cross attention as q GEMM + ls_attention + out GEMM (A/B switch)
+_FUSED_XATTN = os.environ.get("LS_FUSED_XATTN", "1") != "0"
 
 
 def _ff(h, st, ff1, ff2, ff2p):
@@ -179,6 +181,10 @@ class _Transformer:
             self.q2 = dv.packed_ln(sd[b + ".attn2.to_q.weight"], None, ln(b + ".norm2"))
             self.kv2 = dv.packed(None, w=torch.cat([sd[b + ".attn2.to_k.weight"], sd[b + ".attn2.to_v.weight"]], 0))
             self.o2 = dv.packed(b + ".attn2.to_out.0.weight", b + ".attn2.to_out.0.bias")
+            # norm2 + to_q + SDPA + to_out + residual in one launch at C = 320 (ls_cross_attention_block)
+            self.xa = ops.pack_cross_attention(
+                sd[b + ".attn2.to_q.weight"], *ln(b + ".norm2"), sd[b + ".attn2.to_out.0.weight"],
+                sd[b + ".attn2.to_out.0.bias"], heads, dv.device) if _FUSED_XATTN and c == 320 and heads == 8 else None
         self.ff1 = dv.packed_ln(sd[b + ".ff.net.0.proj.weight"], sd[b + ".ff.net.0.proj.bias"], ln(b + ".norm3"),
                                 geglu=True)
         self.ff2 = dv.packed(b + ".ff.net.2.weight", b + ".ff.net.2.bias")
@@ -210,15 +216,23 @@ class _Transformer:
         h = ops.linear(o, self.o1, res=h, stats_out=st)
         # audio cross attention
         if self.has_audio and audio_rows is not None:
-            q = ops.linear(h, self.q2, ln_stats=st)
             if kv is None:
                 kv = ops.linear(audio_rows, self.kv2)
             L = n_audio_tok
+            if ops.cross_attention_ok(h, self.xa, L, HW):
+                st2 = torch.empty_like(st)
+                h = ops.cross_attention_block(h, st, self.xa, kv, L, HW, st2)
+                st = st2
+                return self._tail(x, h, st, n, H, W, C)
+            q = ops.linear(h, self.q2, ln_stats=st)
             ops.attention(q, kv, kv[:, C:], o, batch=n, z2=1, heads=self.heads, nq=HW, nk=L, head_dim=d,
                           qs=(HW * C, 0, C, d), ks=(L * 2 * C, 0, 2 * C, d), vs=(L * 2 * C, 0, 2 * C, d),
                           os_=(HW * C, 0, C, d))
             h = ops.linear(o, self.o2, res=h, stats_out=st)
-        # GEGLU feed-forward (norm3 folded)
+        return self._tail(x, h, st, n, H, W, C)
+
+    def _tail(self, x, h, st, n, H, W, C):
+        # GEGLU feed-forward (norm3 folded), proj_out + the block input
         h = _ff(h, st, self.ff1, self.ff2, self.ff2p)
         return ops.conv(h.view(n, H, W, C), self.proj_out, res=x, gn_out=True)
 

@@ -191,6 +191,41 @@ def test_attention_d512_rescale(gpu, qscale):
     assert rel_err(o.float().cpu(), ref) < 1.5e-2
 
 
+@pytest.mark.parametrize("n_img,L,hw", [(2, 50, 1024), (3, 64, 256), (1, 7, 128)])
+def test_cross_attention_block(gpu, n_img, L, hw):
+    """ls_cross_attention_block (norm2 + to_q + SDPA over the audio tokens + to_out +
+    residual, one launch; attention.py:174-199) against fp32: y and the row statistics
+    of the stored y rows."""
+    C, H, D = 320, 8, 40
+    M = n_img * hw
+    g = torch.Generator().manual_seed(80 + L)
+    r = lambda *s, sc=1.0: torch.randn(*s, generator=g) * sc
+    x = bf(r(M, C) * 1.5 + 0.3)
+    gamma, beta = 1 + 0.1 * r(C), 0.1 * r(C)
+    wq, wo, bo = r(C, C, sc=C ** -0.5), r(C, C, sc=C ** -0.5), 0.1 * r(C)
+    kv = bf(r(n_img * L, 2 * C))
+    xd, kvd = x.to(torch.bfloat16).to(DEV), kv.to(torch.bfloat16).to(DEV)
+    st = ops.row_stats(xd)
+    pk = ops.pack_cross_attention(wq, gamma, beta, wo, bo, H, DEV)
+    st2 = torch.empty_like(st)
+    assert ops.cross_attention_ok(xd, pk, L, hw)
+    y = ops.cross_attention_block(xd, st, pk, kvd, L, hw, st2).float().cpu()
+    ln = torch.nn.functional.layer_norm(x, (C,), gamma, beta, eps=1e-5)
+    q = (ln @ wq.T).reshape(n_img, hw, H, D).permute(0, 2, 1, 3)
+    k = kv[:, :C].reshape(n_img, L, H, D).permute(0, 2, 1, 3)
+    v = kv[:, C:].reshape(n_img, L, H, D).permute(0, 2, 1, 3)
+    o = _sdpa(q, k, v).permute(0, 2, 1, 3).reshape(M, C)
+    ref = o @ wo.T + bo + x
+    e = rel_err(y, ref)
+    print("cross-attention block rel_err", n_img, L, hw, e)
+    assert e < 1.5e-2
+    # the (mean, rstd) of the stored bf16 y rows (norm3's fold)
+    mean, var = y.double().mean(1), y.double().var(1, unbiased=False)
+    s2 = st2.cpu().double()
+    assert torch.allclose(s2[:, 0], mean, rtol=1e-4, atol=1e-4)
+    assert torch.allclose(s2[:, 1], 1 / torch.sqrt(var + 1e-5), rtol=1e-4)
+
+
 @pytest.mark.parametrize("qscale,N,Nk", [(1.0, 1024, 1024), (3.0, 1024, 1024), (3.0, 777, 1000)])
 def test_attention_d40_rescale_fused_qkv(gpu, qscale, N, Nk):
     """The d = 40 self-attention kernel (attn6, 32x32x16 MFMA) on the UNet's fused q|k|v
