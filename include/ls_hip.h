@@ -119,7 +119,10 @@ int ls_conv2d(const ls_conv_desc* d, void* stream);
  * GEMM (K = 320 / 640 linears; also takes the GroupNorm affine prologue on its
  * register-resident A rows), 2 = register-staged tiled GEMM (affine prologue
  * elsewhere -- callers materialise the affine with ls_groupnorm_apply instead),
- * -1 = invalid descriptor.  Host-only, no launch. */
+ * 3 = halo-tile 3x3 conv (ABI 12: 3x3 / stride 1 / pad 1, Cin % 64 == 0, W in {16, 32,
+ * 64} or a multiple of 64, N % 160 or % 128 == 0; takes the GroupNorm affine + SiLU on
+ * its input, once per pixel, and the dual-source concat), -1 = invalid descriptor.
+ * Host-only, no launch. */
 int ls_conv_path(const ls_conv_desc* d);
 size_t ls_conv_workspace_bytes(const ls_conv_desc* d);
 
@@ -368,7 +371,9 @@ int ls_add_rows(const uint16_t* x, int64_t rows, int32_t C, int32_t ldx, const f
 /* Tuning / A-B switches for ls_conv2d (process-wide, host side only):
  * key 1 = force the register-staged kernel (1) instead of the LDS-DMA one;
  * key 2 = force tile 0 auto, 1 128x128, 2 128x64, 3 64x64, 4 128x32; key 3 = split-K with key 2;
- * key 4 = ablation (1 skip MFMA, 2 skip operand DMA; timing only); key 5 = DMA K-tile depth 32 or 64. */
+ * key 4 = ablation (1 skip MFMA, 2 skip operand DMA; timing only); key 5 = DMA K-tile depth 32 or 64;
+ * key 6 = row-block GEMM on / off; key 7 = its K = 640 instances on / off; key 8 = halo-tile 3x3
+ * conv on / off (ABI 12); key 9 = d = 40 self attention on the 32x32x16 kernel (ABI 12). */
 int ls_set_tuning(int32_t key, int32_t value);
 
 /* Diagnostics: workgroups per CU the runtime can co-schedule for a GEMM kernel

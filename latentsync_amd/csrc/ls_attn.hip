@@ -1893,7 +1893,12 @@ using namespace ls;
 
 static bool g_attn_v1 = getenv("LS_ATTN_V1") != nullptr;  // A/B switch: force the 16-query kernel
 static bool g_attn_v3 = getenv("LS_ATTN_V3") != nullptr;  // A/B switch: attn3 for d = 40 too
-static bool g_attn5 = getenv("LS_ATTN5") != nullptr;  // A/B switch: d = 40 self attention on attn5 (16x16x32)
+// A/B switch: d = 40 self attention on attn6 (32x32x16); measured 3 % slower than attn5 at 48
+// windows (1670 vs 1620 us per call, profiles/r04b_attn_ab.txt), so attn5 stays the default
+static bool g_attn6 = getenv("LS_ATTN6") != nullptr;
+namespace ls {
+void attn_set_attn6(bool on) { g_attn6 = on; }  // ls_set_tuning key 9
+}
 static bool g_attnw_off = getenv("LS_ATTNW_OFF") != nullptr;  // A/B switch: d = 512 on attn_kernel
 static bool g_seq_valu = getenv("LS_ATTN_SEQ_VALU") != nullptr;  // A/B switch: dot-product short-sequence kernel
 static bool g_seq160_valu = getenv("LS_ATTN_SEQ160_VALU") != nullptr;  // A/B switch: ... for d = 160 only
@@ -1994,7 +1999,7 @@ extern "C" int ls_attention(const ls_attn_desc* d, void* stream) {
     // queries per wave, row sums from the PV MFMA; short key sets (the 50 audio tokens)
     // and other head dims: attn3 (register-staged tiles)
     if (D == 40 && !g_attn_v3 && d->nk > 128 && ((long)(d->nk - 1) * std::max(d->k_si, d->v_si) + D) * 2 < (1L << 31))
-      return g_attn5 ? launch_attn5<2, 3, 40, 4>(a, d->batch, d->heads, s) : launch_attn6<40>(a, d->batch, d->heads, s);
+      return g_attn6 ? launch_attn6<40>(a, d->batch, d->heads, s) : launch_attn5<2, 3, 40, 4>(a, d->batch, d->heads, s);
     if (D == 40) return launch_attn3<2, 3, 40>(a, d->batch, d->heads, s);
     switch ((D + 15) / 16) {
       case 1: case 2: return launch_attn3<1, 2, 0>(a, d->batch, d->heads, s);

@@ -247,14 +247,24 @@ __host__ __device__ constexpr bool cs_tile_fits() {
   return BM != 256 && BM % CS_ROWS == 0 && CS_ROWS % (BM / WM) == 0 && WM * WN * 64 >= BN;
 }
 
-template <int BM, int BN, int WM, int WN, bool GEN>
+// CSF: the column sums also for a 256-row tile whose wave rows are 64 (the halo conv);
+// RW > 0: the tile's rows are BM / RW segments of RW consecutive output pixels, one per
+// image row (the halo conv's TH x TW tiles); m0 is then the tile's VIRTUAL first row
+// (GroupNorm slots) and m0r the real first row.
+template <int BM, int BN, int WM, int WN, bool GEN, bool CSF = false, int RW = 0>
 __device__ __forceinline__ void store_tile_plain(const ConvArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
-                                                 float* st, int m0, int n0) {
+                                                 float* st, int m0, int n0, long m0r = 0) {
   constexpr int NT = WM * WN * 64, WTM = BM / WM, SP = BN + 4;
   constexpr int CPRW = BN / 8;                 // chunk columns per tile row
   constexpr int RPI = NT / CPRW;               // rows per iteration
   constexpr int ITER = (WTM + RPI - 1) / RPI;  // iterations per wave-row pass
-  constexpr bool CSOK = cs_tile_fits<BM, BN, WM, WN>();
+  constexpr bool CSOK = CSF || cs_tile_fits<BM, BN, WM, WN>();
+  static_assert(!CSF || (CS_ROWS % WTM == 0 && NT >= BN), "column-sum slots of whole wave rows");
+  // tile-local row -> output row
+  auto out_row = [&](int lr) -> int {
+    if constexpr (RW > 0) return (int)(m0r + (long)(lr / RW) * a.Wo + lr % RW);
+    else return m0 + lr;
+  };
   const int tid = threadIdx.x;
   const int c8 = (tid % CPRW) * 8, r0 = tid / CPRW;
   const int col = n0 + c8;
@@ -264,14 +274,15 @@ __device__ __forceinline__ void store_tile_plain(const ConvArgs& a, f32x4 (&acc)
   // row vector (per-frame temb / positional-encoding rows): one row for the whole
   // tile in the common case (rows_per_vec >= the tile's row span), folded into
   // the per-column constants; otherwise looked up per row.
-  const bool rv_tile = a.rowvec && m0 / a.rows_per_vec == (min(m0 + BM, a.M) - 1) / a.rows_per_vec;
+  const bool rv_tile = a.rowvec && out_row(0) / a.rows_per_vec == (RW > 0 ? out_row(BM - 1)
+                                                                           : min(m0 + BM, a.M) - 1) / a.rows_per_vec;
   float bb[8], cs[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { bb[j] = 0.f; cs[j] = 0.f; }
   if (cok && a.bias) load8f(a.bias + col, bb);
   if (cok && rv_tile) {
     float rv[8];
-    load8f(a.rowvec + rv_row(a, m0) + col, rv);
+    load8f(a.rowvec + rv_row(a, out_row(0)) + col, rv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) bb[j] += rv[j];
   }
@@ -279,12 +290,11 @@ __device__ __forceinline__ void store_tile_plain(const ConvArgs& a, f32x4 (&acc)
 #pragma unroll 1
   for (int p = 0; p < WM; ++p) {
     stage_acc<BM, BN, WM, WN>(acc, st, p);
-    const int rbase = m0 + p * WTM;
     float2 mr[ITER];
     uint4 rs[ITER];
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
-      const int rl = r0 + it * RPI, row = rbase + rl;
+      const int rl = r0 + it * RPI, row = out_row(p * WTM + rl);
       const bool ok = cok && rl < WTM && row < a.M;
       mr[it] = make_float2(0.f, 1.f);
       rs[it] = make_uint4(0, 0, 0, 0);
@@ -294,7 +304,7 @@ __device__ __forceinline__ void store_tile_plain(const ConvArgs& a, f32x4 (&acc)
     __syncthreads();
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
-      const int rl = r0 + it * RPI, row = rbase + rl;
+      const int rl = r0 + it * RPI, row = out_row(p * WTM + rl);
       if (!(cok && rl < WTM && row < a.M)) continue;
       const float* s = st + rl * SP + c8;
       const float4 s0 = *(const float4*)s, s1 = *(const float4*)(s + 4);
@@ -1823,6 +1833,265 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
   }
 }
 
+// ------------------------------------------------------------- halo-tile 3x3 conv
+// conv3x3_halo_kernel: 3x3 / stride 1 / pad 1 convolutions with Cin % 64 == 0 whose A
+// operand comes from an LDS HALO TILE.  The implicit-GEMM kernels above gather A per tap:
+// a 64-channel chunk of every output pixel's 3x3 window is DMA'd 9 times (9 K-tiles), so
+// at N = 128 / 160 the operand DMA -- about 60 issue cycles per 1-KB wave-instruction --
+// outweighs the MFMAs it feeds (the VAE's 128-channel convs at 256^2 ran at 0.34 of the
+// bf16 peak), and a GroupNorm affine + SiLU on the input had to be materialised by its
+// own pass (ls_groupnorm_apply) because applying it in the gather would repeat it 9 times.
+// Here a block owns a TH x TW patch of one image (256 output pixels) x BN output channels:
+//   * per 64-channel chunk, the (TH + 2) x (TW + 2) input pixels of the patch are loaded
+//     ONCE (buffer loads into registers; pixels outside the image read zeros), optionally
+//     put through y = silu?(x * scale + shift) (the GroupNorm affine of the pixel's sample)
+//     and stored to a halo image in LDS: 128 B per pixel, the 16-B chunks XOR-swizzled by
+//     (pixel & 7) -- conflict-free ds_read_b128 fragment reads at ANY pixel offset, which
+//     the 9 taps need (brute-forced over the lane groups; the GEMMs' ((row >> 1) & 7)
+//     swizzle is 2-way there).  Halo rows are TW + 8 pixels long (== 0 mod 8), so the
+//     swizzle phase of every fragment of a wave equals its first fragment's: one address
+//     computation per (tap, k-step) and lane, fragment offsets are immediates;
+//   * the 9 taps of the chunk then run from that image: tap (kh, kw) shifts the read by
+//     kh (TW + 8) + kw pixels; the weight K-tile of each tap ([BN][64], channel-chunk-major
+//     packing) streams through an NSW-slot LDS ring by LDS-DMA, NSW - 1 taps ahead;
+//   * the halo of chunk c + 1 is loaded into registers at tap 0 of chunk c and written to
+//     the other halo image at tap 8 (so the input affine's VALU work overlaps the MFMAs
+//     of 8 taps); every wait is one constant vmcnt (padded dummy DMAs).
+// 8 waves as 4 (pixels) x 2 (channels), 64 x BN/2 per wave; the epilogue is
+// store_tile_plain (bias, per-frame row vector, residual, scale, GroupNorm column sums
+// of the output) with the patch's rows mapped back to image rows.
+template <int TW, int BN>
+struct HaloCfg {
+  static constexpr int TH = 256 / TW;
+  static constexpr int P = TW + 8;                       // halo row pitch (pixels), 0 mod 8
+  static constexpr int HALO = (TH + 2) * P * 8;          // uint4 per halo image
+  static constexpr int WSLOT = BN * 8;                   // uint4 per weight ring slot (BN x 64 k)
+  static constexpr int NSW = BN <= 128 ? 3 : 2;          // weight ring slots
+  static constexpr int NHL = (HALO + 511) / 512;         // halo loads per thread per chunk
+  static constexpr int DPT = (WSLOT + 511) / 512;        // weight DMAs per thread per tap
+  static constexpr int FN = BN / 32;                     // 16-column fragments per wave
+  static constexpr size_t SHM = ((size_t)2 * HALO + (size_t)NSW * WSLOT + 64 + 64) * 16;  // + dummy, affine
+  static_assert(SHM <= 163840, "halo conv LDS");
+  static_assert((size_t)64 * (BN + 4) * 4 <= (size_t)2 * HALO * 16, "epilogue staging fits the halo images");
+};
+
+__device__ i32x4 ls_raw_buffer_load_v4(i32x4 rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.load.v4i32");
+
+// halo loads of a chunk in 3 batches (pieces [hb_lo(b), hb_lo(b + 1))): loaded at taps 0 /
+// 3 / 6 of the previous chunk and stored at taps 3 / 6 / 8, so at most 3 pieces (12 VGPRs)
+// are in flight per thread
+__host__ __device__ constexpr int hb_lo(int b, int nhl) { return b == 0 ? 0 : b == 1 ? (nhl + 2) / 3 : b == 2 ? (2 * nhl + 2) / 3 : nhl; }
+// VMEM instructions a thread issues after the weight DMA at tap t (0..8) of a chunk:
+// the halo batch loaded there (+ its 4 affine loads) when a next chunk exists
+// the halo batch loaded there (+ at tap 0 the chunk's affine parameters, one float4 per thread)
+__host__ __device__ constexpr int halo_issue(int t, int nhl, bool gn) {
+  return t == 0 ? hb_lo(1, nhl) + (gn ? 1 : 0) : t == 3 ? hb_lo(2, nhl) - hb_lo(1, nhl) : t == 6 ? nhl - hb_lo(2, nhl) : 0;
+}
+
+template <int TW, int BN, bool GN, bool CSF>
+__global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
+  using HC = HaloCfg<TW, BN>;
+  constexpr int TH = HC::TH, P = HC::P, HALO = HC::HALO, WSLOT = HC::WSLOT, NSW = HC::NSW;
+  constexpr int NHL = HC::NHL, DPT = HC::DPT, FM = 4, FN = HC::FN, WTN = BN / 2;
+  constexpr int HB = (NHL + 2) / 3;  // largest batch
+  extern __shared__ __attribute__((aligned(16))) uint4 lds_dyn[];
+  uint4* const hbuf = lds_dyn;                 // [2][HALO]
+  uint4* const wbuf = lds_dyn + 2 * HALO;      // [NSW][WSLOT]
+  uint4* const dummy = wbuf + NSW * WSLOT;     // 1 KB: padding DMAs land here
+  float4* const gpar = (float4*)(dummy + 64);  // [2 chunk parities][scale 16 | shift 16] float4
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int l16 = lane & 15, lg = lane >> 4;
+  const int ntn = a.N / BN, tpr = a.W / TW, tpc = a.H / TH;
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tn = bid % ntn;
+  bid /= ntn;
+  const int txb = bid % tpr;
+  bid /= tpr;
+  const int tyb = bid % tpc;
+  const int img = bid / tpc;
+  const int y0 = tyb * TH, x0 = txb * TW, n0 = tn * BN;
+  const long HW = (long)a.H * a.W;
+  const int nchunk = a.Cin / 64;
+  const int G = 9 * nchunk;  // taps in all
+
+  // ---- this thread's halo pieces: q = j*512 + tid -> pixel q / 8 = 64 j + tid / 8, logical
+  // 16-B chunk tid & 7; the swizzled slot is j*512 + hdst0 (64 j == 0 mod 8 keeps the phase)
+  const int hc8 = tid & 7;
+  const int hdst0 = (tid >> 3) * 8 + (hc8 ^ ((tid >> 3) & 7));
+  int hpix[NHL];  // pixel index within the image, or -1 (outside: zeros)
+#pragma unroll
+  for (int j = 0; j < NHL; ++j) {
+    const int q = j * 512 + tid, hp = q >> 3;
+    const int hr = hp / P, hcol = hp - hr * P;
+    const int y = y0 - 1 + hr, x = x0 - 4 + hcol;
+    const bool ok = q < HALO && hcol >= 3 && hcol <= TW + 4 && y >= 0 && y < a.H && x >= 0 && x < a.W;
+    hpix[j] = ok ? y * a.W + x : -1;
+  }
+  const uint32_t cap = 0x7FFFFFFFu;
+  const i32x4 rs1 = buffer_rsrc(a.x1 + img * HW * a.ld1, (uint32_t)min((long)HW * a.ld1 * 2, (long)cap));
+  const i32x4 rs2 = a.C2 ? buffer_rsrc(a.x2 + img * HW * a.ld2, (uint32_t)min((long)HW * a.ld2 * 2, (long)cap)) : rs1;
+  const long aff0 = (long)img * HW / a.pix_per_sample * a.Cin;
+  uint4 hreg[HB];
+  float4 gp;
+  // the affine parameters of chunk ci (64 scales, 64 shifts): every thread loads one float4
+  // (the same count per wave), threads 0..31 keep theirs in LDS for store_halo
+  auto load_par = [&](int ci) {
+    const int k = tid & 31;
+    gp = *(const float4*)((k < 16 ? a.aff_scale : a.aff_shift) + aff0 + ci * 64 + (k & 15) * 4);
+  };
+  auto store_par = [&](int ci) {
+    if (tid < 32) gpar[(ci & 1) * 32 + tid] = gp;
+  };
+  auto load_halo = [&](int ci, int b) {
+    const bool two = ci * 64 >= a.C1;
+    const int ld = two ? a.ld2 : a.ld1;
+    const int soff = (two ? ci * 64 - a.C1 : ci * 64) * 2;
+    const int j0 = hb_lo(b, NHL), j1 = hb_lo(b + 1, NHL);
+#pragma unroll
+    for (int j = j0; j < j1; ++j) {
+      const int vo = hpix[j] >= 0 ? hpix[j] * ld * 2 + hc8 * 16 : (int)0x80000000;
+      hreg[j - j0] = __builtin_bit_cast(uint4, ls_raw_buffer_load_v4(two ? rs2 : rs1, vo, soff, 0));
+    }
+    if constexpr (GN) {
+      if (b == 0 && ci > 0) load_par(ci);
+    }
+  };
+  auto store_halo = [&](int buf, int b) {
+    uint4* dst = hbuf + buf * HALO + hdst0;
+    const int j0 = hb_lo(b, NHL), j1 = hb_lo(b + 1, NHL);
+    float4 gsc[2], gsh[2];
+    if constexpr (GN) {  // this thread's 8 channels (chunk parity buf)
+      const float4* gq = gpar + buf * 32 + hc8 * 2;
+      gsc[0] = gq[0]; gsc[1] = gq[1]; gsh[0] = gq[16]; gsh[1] = gq[17];
+    }
+#pragma unroll
+    for (int j = j0; j < j1; ++j) {
+      if (j * 512 + tid >= HALO) continue;
+      uint4 v = hreg[j - j0];
+      if constexpr (GN) {
+        if (hpix[j] >= 0) {  // zero padding stays zero: the conv pads the ACTIVATED input
+          float f[8];
+          unpack8(v, f);
+          const float scl[8] = {gsc[0].x, gsc[0].y, gsc[0].z, gsc[0].w, gsc[1].x, gsc[1].y, gsc[1].z, gsc[1].w};
+          const float shf[8] = {gsh[0].x, gsh[0].y, gsh[0].z, gsh[0].w, gsh[1].x, gsh[1].y, gsh[1].z, gsh[1].w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float t = fmaf(f[e], scl[e], shf[e]);
+            f[e] = a.silu_in ? silu(t) : t;
+          }
+          v = pack8(f);
+        }
+      }
+      dst[j * 512] = v;
+    }
+  };
+
+  // ---- weight DMA: tap g = 9 ci + t is K-tile g of the channel-chunk-major packing
+  int wofs[DPT];
+#pragma unroll
+  for (int j = 0; j < DPT; ++j) {
+    const int q = j * 512 + tid, row = q >> 3, pc = q & 7;
+    const int lc = pc ^ ((row >> 1) & 7);
+    wofs[j] = (n0 + (q < WSLOT ? row : 0)) * a.K + lc * 8;
+  }
+  auto issue_w = [&](int g) {
+    uint4* slot = wbuf + (g % NSW) * WSLOT;
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) {
+      const bool live = j * 512 + wid * 64 < WSLOT;  // wave-uniform
+      glds16(a.w + wofs[j] + (long)g * 64, live ? slot + j * 512 + wid * 64 : dummy);
+    }
+  };
+
+  // ---- A fragment addressing: output pixel p = 64 wm + 16 i + l16 of the patch
+  const int p0 = 64 * wm + l16;
+  const int hp0 = (p0 / TW) * P + (p0 % TW) + 3;  // halo pixel of fragment 0 at tap (0, 0)
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // prologue: weights of taps 0 .. NSW - 2, halo of chunk 0
+  for (int g = 0; g < NSW - 1 && g < G; ++g) issue_w(g);
+  if constexpr (GN) {
+    load_par(0);
+    store_par(0);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    load_halo(0, b);
+    store_halo(0, b);  // (the compiler waits for the loads)
+  }
+
+  auto tap = [&](int ci, auto t_tag, auto last_tag) {
+    constexpr int t = decltype(t_tag)::value;
+    constexpr bool LAST = decltype(last_tag)::value;  // no next chunk
+    const int g = 9 * ci + t;
+    // the weight DMA of tap g landed: VMEM instructions younger than it are the weights
+    // of the NSW - 2 later taps and the halo batches issued at taps t - NSW + 1 .. t - 1
+    constexpr int HY = LAST ? 0 : (t - 1 >= 0 ? halo_issue(t - 1, NHL, GN) : 0) +
+                                  (NSW >= 3 && t - 2 >= 0 ? halo_issue(t - 2, NHL, GN) : 0);
+    if (g + NSW - 2 >= G) wait_vm<0>();  // the ring's tail
+    else wait_vm<(NSW - 2) * DPT + HY>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (g + NSW - 1 < G) issue_w(g + NSW - 1);
+    if constexpr (!LAST) {
+      if constexpr (GN && t == 1) store_par(ci + 1);  // read at taps 3 / 6 / 8, past a barrier
+      if constexpr (t == 3 || t == 6) store_halo((ci + 1) & 1, t / 3 - 1);
+      if constexpr (t == 0 || t == 3 || t == 6) load_halo(ci + 1, t / 3);
+    }
+    const uint4* hb = hbuf + (ci & 1) * HALO;
+    const uint4* wb = wbuf + (g % NSW) * WSLOT;
+    constexpr int kh = t / 3, kw = t % 3;
+    const int hpt = hp0 + kh * P + kw;
+    const int sw = hpt & 7;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int base = hpt * 8 + ((ks * 4 + lg) ^ sw);
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)  // fragment i: + ((16 i) / TW) rows, + (16 i) % TW pixels
+        af[i] = __builtin_bit_cast(bf16x8, hb[base + 8 * (((16 * i) / TW) * P + (16 * i) % TW)]);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bfr[j] = __builtin_bit_cast(bf16x8, wb[swz_bk<64>(wn * WTN + j * 16 + l16, ks * 4 + lg)]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if constexpr (!LAST && t == 8) store_halo((ci + 1) & 1, 2);
+  };
+  using I0 = std::integral_constant<int, 0>; using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>; using I3 = std::integral_constant<int, 3>;
+  using I4 = std::integral_constant<int, 4>; using I5 = std::integral_constant<int, 5>;
+  using I6 = std::integral_constant<int, 6>; using I7 = std::integral_constant<int, 7>;
+  using I8 = std::integral_constant<int, 8>;
+  auto chunk = [&](int ci, auto last) {
+    tap(ci, I0{}, last); tap(ci, I1{}, last); tap(ci, I2{}, last);
+    tap(ci, I3{}, last); tap(ci, I4{}, last); tap(ci, I5{}, last);
+    tap(ci, I6{}, last); tap(ci, I7{}, last); tap(ci, I8{}, last);
+  };
+  for (int ci = 0; ci + 1 < nchunk; ++ci) chunk(ci, std::false_type{});
+  chunk(nchunk - 1, std::true_type{});
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  // epilogue: virtual rows (GroupNorm slots) = the patch's index within its image x 256
+  const int m0v = (int)(img * HW) + (tyb * tpr + txb) * 256;
+  const long m0r = img * HW + (long)y0 * a.W + x0;
+  store_tile_plain<256, BN, 4, 2, false, CSF, TW>(a, acc, (float*)lds_dyn, m0v, n0, m0r);
+}
+
 // ---------------------------------------------------------------- host side
 static bool g_force_regstage = getenv("LS_GEMM_REGSTAGE") != nullptr;
 // A/B switch: 3x3 weights packed tap-major (packing.py reads the same variable)
@@ -2076,6 +2345,58 @@ static void launch_cfg(const ConvArgs& a, int ks, bool tapu, int grid, hipStream
   }
 }
 
+// ---- halo-tile 3x3 conv dispatch (conv3x3_halo_kernel)
+static bool g_halo = getenv("LS_HALO") == nullptr || atoi(getenv("LS_HALO")) != 0;  // A/B switch: LS_HALO=0
+
+// patch width of the halo conv for this call (0: not taken)
+static int halo_tw(const ls_conv_desc* d, const ConvArgs& a) {
+  if (!g_halo || g_force_tile || g_force_regstage || d->ksize != 3 || a.stride != 1 || a.pad != 1 || a.upsample ||
+      !a.ccm || a.Cin % 64 || a.C1 % 64 || a.K != 9 * a.Cin || a.y_f32 || a.act != LS_ACT_NONE ||
+      a.ln_mr || a.stats_out || a.ldy % 8 || (a.res && a.ldr % 8) || a.Ho != a.H || a.Wo != a.W)
+    return 0;
+  if (a.N % 160 && a.N % 128) return 0;
+  if (a.aff_scale && (a.pix_per_sample % (a.H * a.W) || ((uintptr_t)a.aff_scale | (uintptr_t)a.aff_shift) & 15))
+    return 0;
+  if (((uintptr_t)a.x1 | (uintptr_t)a.x2 | (uintptr_t)a.w) & 15 || a.ld1 % 8 || (a.C2 && a.ld2 % 8)) return 0;
+  // 16 x 16 patches everywhere: the smallest halo overhead ((16 + 2)^2 / 256 = 1.27 input
+  // pixels per output pixel; 32 x 8: 1.33, 64 x 4: 1.55) and no register spills
+  const int tw = (a.W % 16 == 0 && a.H % 16 == 0) ? 16 : 0;
+  if (!tw) return 0;
+  if ((long)a.H * a.W * a.ld1 * 2 >= (1L << 31) || (a.C2 && (long)a.H * a.W * a.ld2 * 2 >= (1L << 31)))
+    return 0;  // per-image buffer descriptors
+  return tw;
+}
+
+template <int TW, int BN, bool GN, bool CSF>
+static void launch_halo3(const ConvArgs& a, hipStream_t s) {
+  using HC = HaloCfg<TW, BN>;
+  const int grid = a.n_img * (a.H / HC::TH) * (a.W / TW) * (a.N / BN);
+  LS_SET_MAX_DYN_SHM((conv3x3_halo_kernel<TW, BN, GN, CSF>), HC::SHM);
+  conv3x3_halo_kernel<TW, BN, GN, CSF><<<grid, 512, HC::SHM, s>>>(a);
+}
+
+template <int TW, int BN>
+static void launch_halo2(const ConvArgs& a, hipStream_t s) {
+  if (a.aff_scale) {
+    if (a.cs_out) launch_halo3<TW, BN, true, true>(a, s);
+    else launch_halo3<TW, BN, true, false>(a, s);
+  } else {
+    if (a.cs_out) launch_halo3<TW, BN, false, true>(a, s);
+    else launch_halo3<TW, BN, false, false>(a, s);
+  }
+}
+
+template <int TW>
+static void launch_halo1(const ConvArgs& a, hipStream_t s) {
+  if (a.N % 160 == 0) launch_halo2<TW, 160>(a, s);
+  else launch_halo2<TW, 128>(a, s);
+}
+
+static void launch_halo(const ConvArgs& a, int tw, hipStream_t s) {
+  (void)tw;  // (16: the only patch width compiled)
+  launch_halo1<16>(a, s);
+}
+
 static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split) {
   if (!d || !d->x1 || !d->w || !d->y) return fail(LS_ERR_INVALID, "ls_conv2d: null pointer");
   if (d->ksize != 1 && d->ksize != 3) return fail(LS_ERR_INVALID, "ls_conv2d: ksize must be 1 or 3");
@@ -2144,6 +2465,8 @@ static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split
 
 using namespace ls;
 
+namespace ls { void attn_set_attn6(bool on); }
+
 extern "C" int ls_set_tuning(int32_t key, int32_t value) {
   switch (key) {
     case 1: g_force_regstage = value != 0; return LS_OK;
@@ -2153,6 +2476,8 @@ extern "C" int ls_set_tuning(int32_t key, int32_t value) {
     case 5: if (value != 32 && value != 64) return fail(LS_ERR_INVALID, "BK 32 or 64"); g_bk = value; return LS_OK;
     case 6: g_rowblock = value != 0; return LS_OK;
     case 7: g_rowblock640 = value != 0; return LS_OK;
+    case 8: g_halo = value != 0; return LS_OK;
+    case 9: attn_set_attn6(value != 0); return LS_OK;
     default: return fail(LS_ERR_INVALID, "ls_set_tuning: unknown key");
   }
 }
@@ -2200,6 +2525,10 @@ extern "C" int ls_conv2d(const ls_conv_desc* d, void* stream) {
     if (split > 1) a.partial = (float*)d->workspace;
   }
   hipStream_t s = (hipStream_t)stream;
+  if (const int tw = halo_tw(d, a)) {  // 3x3 from an LDS halo tile, input affine fused, with the column sums
+    launch_halo(a, tw, s);
+    return check_launch("conv3x3_halo_kernel");
+  }
   float* cs = a.cs_out;  // GroupNorm column sums: epilogue (tiled / row-block) or a trailing read pass
   if (rowblock_ok(d, a)) {
     if (launch_rowblock(a, s)) return check_launch("gemm_rowblock_kernel");  // with cs_out if given
@@ -2258,6 +2587,7 @@ extern "C" int ls_conv_path(const ls_conv_desc* d) {
   a.cs_out = nullptr;  // (the column sums never change the path)
   int ntm, ntn;
   if (rowblock_ok(d, a) && rowblock_flags(a, &ntm, &ntn) >= 0) return 1;
+  if (halo_tw(d, a)) return 3;
   return (a.aff_scale || g_force_regstage) ? 2 : 0;
 }
 

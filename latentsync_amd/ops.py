@@ -72,9 +72,15 @@ def _ld(t):
     return ld
 
 
+def conv_path(x, pw: Packed, **kw):
+    """Which kernel family ls_conv2d takes for this call (ls_conv_path: 0 tiled, 1 row-block,
+    2 register-staged, 3 halo-tile 3x3) -- host only, nothing is launched."""
+    return conv(x, pw, _path_only=True, **kw)
+
+
 def conv(x, pw: Packed, *, x2=None, aff=None, stride=1, pad=None, upsample=False, out_hw=None, rowvec=None,
          res=None, out_scale=1.0, act=ACT_NONE, out=None, out_f32=False, split_k=0, ln_stats=None,
-         stats_out=None, gn_out=False, aff_materialize=False):
+         stats_out=None, gn_out=False, aff_materialize=False, _path_only=False):
     """Fused conv/linear.  x (n, H, W, C1) [+ x2 (n, H, W, C2)] -> (n, Ho, Wo, n_out).
     aff = (scale[S][C], shift[S][C], imgs_per_sample, silu); rowvec = (t[S][ld], rows_per_vec, ld[, mod]);
     ln_stats = (mean, rstd) rows from row_stats(): LayerNorm folded into pw (pw.colsum);
@@ -128,6 +134,8 @@ def conv(x, pw: Packed, *, x2=None, aff=None, stride=1, pad=None, upsample=False
         assert stats_out.dtype == torch.float32 and stats_out.is_contiguous() and stats_out.numel() == 2 * n * Ho * Wo
         assert pw.n_out == pw.N and act != ACT_GEGLU, "row statistics over the real output channels only"
         d.row_stats_out, d.row_stats_eps = _p(stats_out), 1e-5
+    if _path_only:
+        return lib.ls_conv_path(C.byref(d))
     if aff is not None and aff_materialize and lib.ls_conv_path(C.byref(d)) == 2:
         xa = group_norm_apply(x, aff[0], aff[1], n // aff[2], bool(aff[3]), x2=x2)
         return conv(xa, pw, stride=stride, pad=pad, upsample=upsample, out_hw=out_hw, rowvec=rowvec, res=res,

@@ -155,13 +155,15 @@ class _Resnet:
         F = n // B
         pps = F * x.shape[1] * x.shape[2]
         s1 = ops.group_norm(x, self.groups, self.eps, *self.n1, B, x2=x2)
-        a1 = ops.group_norm_apply(x, s1[0], s1[1], B, True, x2=x2)
+        # GN affine + SiLU: applied once per pixel in the halo-tile conv's LDS image where it
+        # takes the call (ls_conv_path 3: 32x32 / 16x16), else materialised (ops.conv)
         # gn_out: GroupNorm statistics of every GN input come from its producer's epilogue
-        h = ops.conv(a1, self.c1, rowvec=(temb_all[:, self.temb_slot:], pps, temb_all.shape[1]), gn_out=True)
+        h = ops.conv(x, self.c1, x2=x2, aff=(s1[0], s1[1], F, True), aff_materialize=True,
+                     rowvec=(temb_all[:, self.temb_slot:], pps, temb_all.shape[1]), gn_out=True)
         s2 = ops.group_norm(h, self.groups, self.eps, *self.n2, B)
-        a2 = ops.group_norm_apply(h, s2[0], s2[1], B, True)
         res = x if self.sc is None else ops.conv(x, self.sc, x2=x2)
-        return ops.conv(a2, self.c2, res=res, out_scale=self.out_scale, gn_out=True)
+        return ops.conv(h, self.c2, aff=(s2[0], s2[1], F, True), aff_materialize=True, res=res,
+                        out_scale=self.out_scale, gn_out=True)
 
 
 class _Transformer:

@@ -49,10 +49,12 @@ class _Res:
     def __call__(self, x):
         n = x.shape[0]
         s1 = ops.group_norm(x, 32, 1e-6, *self.n1, n)
-        h = ops.conv(ops.group_norm_apply(x, s1[0], s1[1], n, True), self.c1, gn_out=True)
+        # GN affine + SiLU fused into the halo-tile 3x3 conv where it takes the call, else
+        # materialised once (ops.conv aff_materialize)
+        h = ops.conv(x, self.c1, aff=(s1[0], s1[1], 1, True), aff_materialize=True, gn_out=True)
         s2 = ops.group_norm(h, 32, 1e-6, *self.n2, n)
         res = x if self.sc is None else ops.conv(x, self.sc)
-        return ops.conv(ops.group_norm_apply(h, s2[0], s2[1], n, True), self.c2, res=res, gn_out=True)
+        return ops.conv(h, self.c2, aff=(s2[0], s2[1], 1, True), aff_materialize=True, res=res, gn_out=True)
 
 
 class _Attn:

@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -x -q -m gpu -k "attention" --timeout 120 --timeout-method thread > gpurun_out/r04b_attn_tests.log 2>&1; rc=$?; tail -3 gpurun_out/r04b_attn_tests.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -x -q -m gpu -k "attention or cross" --timeout 120 --timeout-method thread > gpurun_out/r04b_attn_tests.log 2>&1; rc=$?; tail -3 gpurun_out/r04b_attn_tests.log; [ $rc -ne 0 ] && exit $rc
 for r in 1 2; do
   for v in A B; do
     if [ $v = B ]; then e="LS_ATTN5=1"; else e="LS_NONE=1"; fi
@@ -12,4 +12,5 @@ for r in 1 2; do
   done
 done
 timeout -k 10 300 python -u scripts/step_calls.py 48 256 > gpurun_out/r04b_step_calls_w48.txt 2>&1; rc=$?; head -40 gpurun_out/r04b_step_calls_w48.txt; [ $rc -ne 0 ] && exit $rc
-TAG=r04b bash scripts/final_check.sh
+ROUNDS=1 timeout -k 10 400 bash scripts/r04c.sh > gpurun_out/r04c.log 2>&1; rc=$?; tail -3 gpurun_out/r04c.log; [ $rc -ne 0 ] && exit $rc
+SKIP_HEADLINE=1 TAG=r04b bash scripts/final_check.sh

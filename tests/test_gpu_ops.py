@@ -226,8 +226,9 @@ def test_cross_attention_block(gpu, n_img, L, hw):
     assert torch.allclose(s2[:, 1], 1 / torch.sqrt(var + 1e-5), rtol=1e-4)
 
 
+@pytest.mark.parametrize("kernel", ["attn5", "attn6"])
 @pytest.mark.parametrize("qscale,N,Nk", [(1.0, 1024, 1024), (3.0, 1024, 1024), (3.0, 777, 1000)])
-def test_attention_d40_rescale_fused_qkv(gpu, qscale, N, Nk):
+def test_attention_d40_rescale_fused_qkv(gpu, qscale, N, Nk, kernel):
     """The d = 40 self-attention kernel (attn6, 32x32x16 MFMA) on the UNet's fused q|k|v
     rows (row stride 3C) with keys whose scores grow along the sequence, so the running
     max moves past the lazy-rescale threshold on later tiles (qscale 3: log2-unit logits
@@ -247,8 +248,13 @@ def test_attention_d40_rescale_fused_qkv(gpu, qscale, N, Nk):
     qkv = qkv.to(DEV).reshape(n * L, 3 * C)
     o = torch.empty((n * N, C), dtype=torch.bfloat16, device=DEV)
     st = (L * 3 * C, 0, 3 * C, d)
-    ops.attention(qkv, qkv[:, C:], qkv[:, 2 * C:], o, batch=n, z2=1, heads=heads, nq=N, nk=Nk, head_dim=d, qs=st,
-                  ks=st, vs=st, os_=(N * C, 0, C, d))
+    from latentsync_amd import _lib
+    _lib.load().ls_set_tuning(9, int(kernel == "attn6"))  # the 32x32x16 kernel (A/B option) or attn5
+    try:
+        ops.attention(qkv, qkv[:, C:], qkv[:, 2 * C:], o, batch=n, z2=1, heads=heads, nq=N, nk=Nk, head_dim=d,
+                      qs=st, ks=st, vs=st, os_=(N * C, 0, C, d))
+    finally:
+        _lib.load().ls_set_tuning(9, 0)
     assert rel_err(o.float().cpu().reshape(n, N, C), ref) < 1.5e-2
 
 
