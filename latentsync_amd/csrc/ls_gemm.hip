@@ -438,7 +438,8 @@ template <int BM, int BN, int WM, int WN, int EPI = EPI_ANY>
 __device__ __forceinline__ void store_tile(const ConvArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16], float* st,
                                            int m0, int n0, int z) {
   if constexpr (EPI == EPI_PLAIN) {
-    store_tile_plain<BM, BN, WM, WN, false>(a, acc, st, m0, n0);
+    // (the 4 x 2-wave 256-row tile keeps 64-row wave rows: column sums in its epilogue too)
+    store_tile_plain<BM, BN, WM, WN, false, BM == 256 && WM == 4>(a, acc, st, m0, n0);
     return;
   } else if constexpr (EPI == EPI_GEGLU) {
     store_tile_geglu<BM, BN, WM, WN, false>(a, acc, st, m0, n0);
@@ -2397,6 +2398,11 @@ static void launch_halo(const ConvArgs& a, int tw, hipStream_t s) {
   launch_halo1<16>(a, s);
 }
 
+// 256 x 128 tiles (8 waves as 4 x 2, 64 x 64 each) with a 3-stage LDS ring (147 KB) for the
+// short-K linears (K <= 1280, N % 128 == 0): two K-tiles of operand DMA in flight instead of
+// one.  (A/B switch LS_GEMM_T256=0/1; tile id 260.  256 x 160 would leave 2.5 B pieces per thread.)
+static int g_t256 = getenv("LS_GEMM_T256") ? atoi(getenv("LS_GEMM_T256")) : 0;
+
 static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split) {
   if (!d || !d->x1 || !d->w || !d->y) return fail(LS_ERR_INVALID, "ls_conv2d: null pointer");
   if (d->ksize != 1 && d->ksize != 3) return fail(LS_ERR_INVALID, "ls_conv2d: ksize must be 1 or 3");
@@ -2445,7 +2451,10 @@ static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split
                                   {257, 256}, {258, 256}, {128, 160}, {259, 160}};
     t.bm = tb[g_force_tile][0]; t.bn = tb[g_force_tile][1]; t.split = g_force_split ? g_force_split : 1;
   }
-  a.ntm = cdiv(M, t.bm > 256 ? 256 : t.bm); a.ntn = cdiv(d->N, t.bn);  // 257/258/259 = 256-row kernel variants
+  if (g_t256 && !g_force_tile && d->ksize == 1 && a.ktiles <= 20 && d->N % 128 == 0 && !d->aff_scale &&
+      M % 256 == 0 && d->K == Cin && Cin % 64 == 0 && d->C1 % 64 == 0)
+    t = {260, 128, 1};
+  a.ntm = cdiv(M, t.bm > 256 ? 256 : t.bm); a.ntn = cdiv(d->N, t.bn);  // 257..260 = 256-row kernel variants
   // grouped raster (LS_GEMM_GM=g, g row-bands per group): it cuts the wide linears' L2-miss
   // fetch (GEGLU W1 at 8x8 3.6 -> 1.3 GB per call) but measured +0.4 ms per 32-window step
   // against the column-fastest order over three alternated same-box rounds
@@ -2478,6 +2487,7 @@ extern "C" int ls_set_tuning(int32_t key, int32_t value) {
     case 7: g_rowblock640 = value != 0; return LS_OK;
     case 8: g_halo = value != 0; return LS_OK;
     case 9: attn_set_attn6(value != 0); return LS_OK;
+    case 10: g_t256 = value; return LS_OK;
     default: return fail(LS_ERR_INVALID, "ls_set_tuning: unknown key");
   }
 }
@@ -2554,9 +2564,16 @@ extern "C" int ls_conv2d(const ls_conv_desc* d, void* stream) {
   const bool vec = (a.N % 8 == 0) && (a.ldy % 8 == 0) && (!a.res || a.ldr % 8 == 0);
   // (not the 256-row kernels: compiled in, the sums cost their main loop ~12 % -- they run
   // at the 256-VGPR limit -- against a ~15 us read pass; same-box A/B, scripts/ab_lib.sh)
-  const bool cs_epi = cs && a.split == 1 && vec && !(t.bm == 128 && t.bn == 32) && t.bm != 64 && t.bm < 256;
+  const bool cs_epi = cs && a.split == 1 && vec && !(t.bm == 128 && t.bn == 32) && t.bm != 64 &&
+                      (t.bm < 256 || (t.bm == 260 && epi_kind(a) == EPI_PLAIN));
   if (cs_epi) a.cs_out = cs;
-  if (t.bm == 257 && !a.aff_scale && !g_force_regstage && (d->ksize == 1 || tapu)) {  // phased 256x256
+  if (t.bm == 260) {  // 256 x 128, 3-stage ring (short-K linears)
+    switch (epi_kind(a)) {
+      case EPI_PLAIN: launch_dma1<256, 128, 4, 2, 1, false, 3, 64, EPI_PLAIN, true>(a, grid, s); break;
+      case EPI_GEGLU: launch_dma1<256, 128, 4, 2, 1, false, 3, 64, EPI_GEGLU, true>(a, grid, s); break;
+      default: launch_dma1<256, 128, 4, 2, 1, false, 3, 64, EPI_ANY, true>(a, grid, s);
+    }
+  } else if (t.bm == 257 && !a.aff_scale && !g_force_regstage && (d->ksize == 1 || tapu)) {  // phased 256x256
     if (d->ksize == 1) launch_p8_1<1, false>(a, grid, s);
     else launch_p8_1<3, true>(a, grid, s);
   } else if (t.bm == 258 && !a.aff_scale && !g_force_regstage && (d->ksize == 1 || tapu)) {  // 4-stage BK 32

@@ -41,6 +41,9 @@ def run(tag, reps=20, scale=1):
             kw["res"] = torch.randn(n, H, H, cout, device="cuda").to(torch.bfloat16)
         if "rowvec" in epi:
             kw["rowvec"] = (torch.randn(n // 16, pw.N, device="cuda"), 16 * H * H, pw.N)
+        if "aff" in epi and ks == 3:  # GroupNorm affine + SiLU on the input (halo conv fuses it)
+            kw["aff"] = (torch.rand(n, cin, device="cuda") + 0.5, torch.randn(n, cin, device="cuda") * 0.1, 1, True)
+            kw["aff_materialize"] = True
         if "ln" in epi and ks == 1 and cin <= 2048:
             pw.colsum = pw.w.float().sum(1).contiguous()
             kw["ln_stats"] = ops.row_stats(x.view(-1, cin))
@@ -91,5 +94,7 @@ if __name__ == "__main__":
         lib.ls_set_tuning(5, 32 if "bk32" in parts else 64)
         lib.ls_set_tuning(2, tile[0] if tile else 0)
         lib.ls_set_tuning(6, 0 if "norb" in parts else 1)
+        lib.ls_set_tuning(8, 0 if "nohalo" in parts else 1)
+        lib.ls_set_tuning(10, 1 if "t256" in parts else 0)
         TORCH_REF = "torch" in parts
         run(arg, scale=int(sc or 1))
