@@ -200,6 +200,17 @@ def step_probe(engine, device):
             blocks[-1][2] += fg + fa
         return r
 
+    orig_xa = ops.cross_attention_block
+
+    def cross_attention_block(x2d, ln_stats, pk, kv, L, hw, stats_out, out=None, eps=1e-5):
+        # fused norm2 + to_q + SDPA + to_out (ls_cross_attention_block): the algorithmic
+        # 2*M*C*C (q) + 4*M*heads*L*d (SDPA) + 2*M*C*C (out) FLOPs
+        r = orig_xa(x2d, ln_stats, pk, kv, L, hw, stats_out, out=out, eps=eps)
+        M, C = x2d.shape
+        if depth[0]:
+            blocks[-1][2] += 4.0 * M * C * C + 4.0 * M * C * L
+        return r
+
     orig_ff = ops.feedforward
 
     def feedforward(x2d, ln_stats, w1, w2, w2ff, out=None):
@@ -211,11 +222,13 @@ def step_probe(engine, device):
         return r
 
     ops.conv, ops.attention, ops.temporal_attention, ops.feedforward = conv, attention, temporal_attention, feedforward
+    ops.cross_attention_block = cross_attention_block
     U._Transformer.__call__, U._Motion.__call__ = wrap(orig_t), wrap(orig_m)
     try:
         engine._step()
     finally:
         ops.conv, ops.attention, ops.temporal_attention, ops.feedforward = orig_conv, orig_attn, orig_tattn, orig_ff
+        ops.cross_attention_block = orig_xa
         U._Transformer.__call__, U._Motion.__call__ = orig_t, orig_m
     torch.cuda.synchronize(device)
 

@@ -2355,7 +2355,10 @@ static int halo_tw(const ls_conv_desc* d, const ConvArgs& a) {
       !a.ccm || a.Cin % 64 || a.C1 % 64 || a.K != 9 * a.Cin || a.y_f32 || a.act != LS_ACT_NONE ||
       a.ln_mr || a.stats_out || a.ldy % 8 || (a.res && a.ldr % 8) || a.Ho != a.H || a.Wo != a.W)
     return 0;
-  if (a.N % 160 && a.N % 128) return 0;
+  // N <= 640: with more output channels the patch is re-loaded and re-transformed per N tile
+  // and the tiled 256x256 kernel wins (VAE 512 channels at 32^2: 3667 vs 3409 us; 128 at
+  // 256^2: 18660 vs 23610 us incl. the materialised GroupNorm; profiles/r04f_ab_t256_halo.txt)
+  if ((a.N % 160 && a.N % 128) || a.N > 640) return 0;
   if (a.aff_scale && (a.pix_per_sample % (a.H * a.W) || ((uintptr_t)a.aff_scale | (uintptr_t)a.aff_shift) & 15))
     return 0;
   if (((uintptr_t)a.x1 | (uintptr_t)a.x2 | (uintptr_t)a.w) & 15 || a.ld1 % 8 || (a.C2 && a.ld2 % 8)) return 0;
