@@ -427,8 +427,8 @@ __global__ void __launch_bounds__(256, (KC >= 5 && !ONE) ? 1 : 2) attn3_kernel(A
         const int d = nd * 16 + 4 * lg;
         if (d + 3 < a.D) {
           uint2 w;
-          w.x = (uint32_t)f2bf(oacc[g][nd][0] * inv) | ((uint32_t)f2bf(oacc[g][nd][1] * inv) << 16);
-          w.y = (uint32_t)f2bf(oacc[g][nd][2] * inv) | ((uint32_t)f2bf(oacc[g][nd][3] * inv) << 16);
+          w.x = pack2(oacc[g][nd][0] * inv, oacc[g][nd][1] * inv);
+          w.y = pack2(oacc[g][nd][2] * inv, oacc[g][nd][3] * inv);
           *(uint2*)(orow + d) = w;
         } else {
 #pragma unroll
@@ -699,8 +699,8 @@ __global__ void __launch_bounds__(256, 2) attn5_kernel(AttnArgs a, int nqb, int 
         const int d = nd * 16 + 4 * lg;
         if (d + 3 < a.D) {
           uint2 w;
-          w.x = (uint32_t)f2bf(oacc[g][nd][0] * inv) | ((uint32_t)f2bf(oacc[g][nd][1] * inv) << 16);
-          w.y = (uint32_t)f2bf(oacc[g][nd][2] * inv) | ((uint32_t)f2bf(oacc[g][nd][3] * inv) << 16);
+          w.x = pack2(oacc[g][nd][0] * inv, oacc[g][nd][1] * inv);
+          w.y = pack2(oacc[g][nd][2] * inv, oacc[g][nd][3] * inv);
           *(uint2*)(orow + d) = w;
         } else {
 #pragma unroll
@@ -1855,8 +1855,8 @@ __global__ void __launch_bounds__(256, OCC) attn8_kernel(AttnArgs a, const uint8
         const int d = nd * 16 + 4 * lg;
         if (d + 3 < D) {
           uint2 w;
-          w.x = (uint32_t)f2bf(oacc[g][nd][0] * inv) | ((uint32_t)f2bf(oacc[g][nd][1] * inv) << 16);
-          w.y = (uint32_t)f2bf(oacc[g][nd][2] * inv) | ((uint32_t)f2bf(oacc[g][nd][3] * inv) << 16);
+          w.x = pack2(oacc[g][nd][0] * inv, oacc[g][nd][1] * inv);
+          w.y = pack2(oacc[g][nd][2] * inv, oacc[g][nd][3] * inv);
           *(uint2*)(orow + d) = w;
         }
       }

@@ -41,8 +41,13 @@ __device__ __forceinline__ u16 f2bf(float f) {
   return __builtin_bit_cast(u16, b);
 }
 
+// two floats -> one dword of bf16 (a low): ONE v_cvt_pk_bf16_f32 on both.  (Two scalar
+// casts combined with shift / or compile to 2 converts + v_lshlrev + v_or_sdwa.)
+typedef __bf16 bf16x2_cv __attribute__((ext_vector_type(2)));
+typedef float f32x2_cv __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  const f32x2_cv v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_cv));
 }
 
 __device__ __forceinline__ void unpack8(const uint4& v, float* f) {
@@ -68,6 +73,12 @@ __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_ex
 // (__frcp_rn is the correctly rounded reciprocal: a 10-instruction division sequence.)
 __device__ __forceinline__ float silu(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + fast_exp2(x * -1.4426950408889634f));
+}
+// silu(t) from u = t log2(e) (a producer that folds log2(e) into its affine): 5 VALU with
+// the affine's fma -- e = 2^-u, r = 1 / ((1 + e) log2 e) by one fma + v_rcp_f32, u r = t / (1 + e^-t)
+__device__ __forceinline__ float silu_log2(float u) {
+  const float e = fast_exp2(-u);
+  return u * __builtin_amdgcn_rcpf(fmaf(e, 1.4426950408889634f, 1.4426950408889634f));
 }
 
 // exact-erf GELU (diffusers GEGLU / whisper MLP) with a branch-free erf:

@@ -2003,11 +2003,16 @@ __host__ __device__ constexpr int halo_issue(int t, int nhl, bool gn) {
   return t == 0 ? hb_lo(1, nhl) + (gn ? 1 : 0) : t == 3 ? hb_lo(2, nhl) - hb_lo(1, nhl) : t == 6 ? nhl - hb_lo(2, nhl) : 0;
 }
 
-template <int TW, int BN, bool GN, bool CSF>
+// RP: the halo pieces are enumerated over the (TH + 2) x (TW + 2) pixels the taps read
+// (2592 pieces for 16 x 16: 5.06 per thread) instead of over the padded image
+// (HALO = 3456: 6.75), so a wave transforms ~25 % fewer pieces; each piece's LDS slot is
+// then per piece (hdst[]), not one base + j * 512
+template <int TW, int BN, bool GN, bool CSF, bool RP = false>
 __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
   using HC = HaloCfg<TW, BN>;
   constexpr int TH = HC::TH, P = HC::P, HALO = HC::HALO, WSLOT = HC::WSLOT, NSW = HC::NSW;
-  constexpr int NHL = HC::NHL, DPT = HC::DPT, FM = 4, FN = HC::FN, WTN = BN / 2;
+  constexpr int NPC = RP ? (TH + 2) * (TW + 2) * 8 : HALO;  // pieces per chunk
+  constexpr int NHL = (NPC + 511) / 512, DPT = HC::DPT, FM = 4, FN = HC::FN, WTN = BN / 2;
   constexpr int HB = (NHL + 2) / 3;  // largest batch
   extern __shared__ __attribute__((aligned(16))) uint4 lds_dyn[];
   uint4* const hbuf = lds_dyn;                 // [2][HALO]
@@ -2036,13 +2041,22 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
   const int hc8 = tid & 7;
   const int hdst0 = (tid >> 3) * 8 + (hc8 ^ ((tid >> 3) & 7));
   int hpix[NHL];  // pixel index within the image, or -1 (outside: zeros)
+  int hdst[RP ? NHL : 1];
 #pragma unroll
   for (int j = 0; j < NHL; ++j) {
     const int q = j * 512 + tid, hp = q >> 3;
-    const int hr = hp / P, hcol = hp - hr * P;
-    const int y = y0 - 1 + hr, x = x0 - 4 + hcol;
-    const bool ok = q < HALO && hcol >= 3 && hcol <= TW + 4 && y >= 0 && y < a.H && x >= 0 && x < a.W;
-    hpix[j] = ok ? y * a.W + x : -1;
+    if constexpr (RP) {
+      const int hr = hp / (TW + 2), hcol = hp - hr * (TW + 2);
+      const int y = y0 - 1 + hr, x = x0 - 1 + hcol;
+      const int slot = hr * P + hcol + 3;
+      hdst[j] = slot * 8 + (hc8 ^ (slot & 7));
+      hpix[j] = q < NPC && y >= 0 && y < a.H && x >= 0 && x < a.W ? y * a.W + x : -1;
+    } else {
+      const int hr = hp / P, hcol = hp - hr * P;
+      const int y = y0 - 1 + hr, x = x0 - 4 + hcol;
+      const bool ok = q < HALO && hcol >= 3 && hcol <= TW + 4 && y >= 0 && y < a.H && x >= 0 && x < a.W;
+      hpix[j] = ok ? y * a.W + x : -1;
+    }
   }
   const uint32_t cap = 0x7FFFFFFFu;
   const i32x4 rs1 = buffer_rsrc(a.x1 + img * HW * a.ld1, (uint32_t)min((long)HW * a.ld1 * 2, (long)cap));
@@ -2056,8 +2070,9 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
     const int k = tid & 31;
     gp = *(const float4*)((k < 16 ? a.aff_scale : a.aff_shift) + aff0 + ci * 64 + (k & 15) * 4);
   };
-  auto store_par = [&](int ci) {
-    if (tid < 32) gpar[(ci & 1) * 32 + tid] = gp;
+  auto store_par = [&](int ci) {  // scale and shift times log2(e): store_halo applies silu_log2
+    constexpr float L2E = 1.4426950408889634f;
+    if (tid < 32) gpar[(ci & 1) * 32 + tid] = make_float4(gp.x * L2E, gp.y * L2E, gp.z * L2E, gp.w * L2E);
   };
   auto load_halo = [&](int ci, int b) {
     const bool two = ci * 64 >= a.C1;
@@ -2074,7 +2089,8 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
     }
   };
   auto store_halo = [&](int buf, int b) {
-    uint4* dst = hbuf + buf * HALO + hdst0;
+    uint4* const hb0 = hbuf + buf * HALO;
+    uint4* dst = hb0 + hdst0;
     const int j0 = hb_lo(b, NHL), j1 = hb_lo(b + 1, NHL);
     float4 gsc[2], gsh[2];
     if constexpr (GN) {  // this thread's 8 channels (chunk parity buf)
@@ -2083,7 +2099,7 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
     }
 #pragma unroll
     for (int j = j0; j < j1; ++j) {
-      if (j * 512 + tid >= HALO) continue;
+      if (j * 512 + tid >= NPC) continue;
       uint4 v = hreg[j - j0];
       if constexpr (GN) {
         if (hpix[j] >= 0) {  // zero padding stays zero: the conv pads the ACTIVATED input
@@ -2092,31 +2108,33 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
           const float scl[8] = {gsc[0].x, gsc[0].y, gsc[0].z, gsc[0].w, gsc[1].x, gsc[1].y, gsc[1].z, gsc[1].w};
           const float shf[8] = {gsh[0].x, gsh[0].y, gsh[0].z, gsh[0].w, gsh[1].x, gsh[1].y, gsh[1].z, gsh[1].w};
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float t = fmaf(f[e], scl[e], shf[e]);
-            f[e] = a.silu_in ? silu(t) : t;
-          }
+          for (int e = 0; e < 8; ++e) f[e] = silu_log2(fmaf(f[e], scl[e], shf[e]));  // (host: GN implies SiLU)
           v = pack8(f);
         }
       }
-      dst[j * 512] = v;
+      if constexpr (RP) hb0[hdst[j]] = v;
+      else dst[j * 512] = v;
     }
   };
 
   // ---- weight DMA: tap g = 9 ci + t is K-tile g of the channel-chunk-major packing
-  int wofs[DPT];
+  // (buffer-descriptor DMA from column n0: per thread one byte offset, per tap the uniform
+  // soffset g * 128 -- no 64-bit address arithmetic in the tap loop)
+  const i32x4 rs_w = buffer_rsrc(a.w + (long)n0 * a.K, (uint32_t)min((long)BN * a.K * 2, (long)cap));
+  int wvo[DPT];
 #pragma unroll
   for (int j = 0; j < DPT; ++j) {
     const int q = j * 512 + tid, row = q >> 3, pc = q & 7;
     const int lc = pc ^ ((row >> 1) & 7);
-    wofs[j] = (n0 + (q < WSLOT ? row : 0)) * a.K + lc * 8;
+    wvo[j] = ((q < WSLOT ? row : 0) * a.K + lc * 8) * 2;
   }
   auto issue_w = [&](int g) {
     uint4* slot = wbuf + (g % NSW) * WSLOT;
 #pragma unroll
     for (int j = 0; j < DPT; ++j) {
       const bool live = j * 512 + wid * 64 < WSLOT;  // wave-uniform
-      glds16(a.w + wofs[j] + (long)g * 64, live ? slot + j * 512 + wid * 64 : dummy);
+      ls_raw_buffer_load_lds(rs_w, (__attribute__((address_space(3))) void*)(live ? slot + j * 512 + wid * 64 : dummy), 16,
+                             wvo[j], g * 128, 0, 0);
     }
   };
 
@@ -2476,6 +2494,7 @@ static void launch_cfg(const ConvArgs& a, int ks, bool tapu, int grid, hipStream
 
 // ---- halo-tile 3x3 conv dispatch (conv3x3_halo_kernel)
 static bool g_halo = getenv("LS_HALO") == nullptr || atoi(getenv("LS_HALO")) != 0;  // A/B switch: LS_HALO=0
+static bool g_halo_rp = getenv("LS_HALO_RP") != nullptr;  // A/B switch: halo pieces over the read pixels only
 
 // patch width of the halo conv for this call (0: not taken)
 static int halo_tw(const ls_conv_desc* d, const ConvArgs& a) {
@@ -2487,8 +2506,8 @@ static int halo_tw(const ls_conv_desc* d, const ConvArgs& a) {
   // and the tiled 256x256 kernel wins (VAE 512 channels at 32^2: 3667 vs 3409 us; 128 at
   // 256^2: 18660 vs 23610 us incl. the materialised GroupNorm; profiles/r04f_ab_t256_halo.txt)
   if ((a.N % 160 && a.N % 128) || a.N > 640) return 0;
-  if (a.aff_scale && (a.pix_per_sample % (a.H * a.W) || ((uintptr_t)a.aff_scale | (uintptr_t)a.aff_shift) & 15))
-    return 0;
+  if (a.aff_scale && (!a.silu_in || a.pix_per_sample % (a.H * a.W) || ((uintptr_t)a.aff_scale | (uintptr_t)a.aff_shift) & 15))
+    return 0;  // (the kernel's input transform is the GroupNorm affine + SiLU of a ResnetBlock)
   if (((uintptr_t)a.x1 | (uintptr_t)a.x2 | (uintptr_t)a.w) & 15 || a.ld1 % 8 || (a.C2 && a.ld2 % 8)) return 0;
   // 16 x 16 patches everywhere: the smallest halo overhead ((16 + 2)^2 / 256 = 1.27 input
   // pixels per output pixel; 32 x 8: 1.33, 64 x 4: 1.55) and no register spills
@@ -2499,19 +2518,24 @@ static int halo_tw(const ls_conv_desc* d, const ConvArgs& a) {
   return tw;
 }
 
-template <int TW, int BN, bool GN, bool CSF>
+template <int TW, int BN, bool GN, bool CSF, bool RP = false>
 static void launch_halo3(const ConvArgs& a, hipStream_t s) {
   using HC = HaloCfg<TW, BN>;
   const int grid = a.n_img * (a.H / HC::TH) * (a.W / TW) * (a.N / BN);
-  LS_SET_MAX_DYN_SHM((conv3x3_halo_kernel<TW, BN, GN, CSF>), HC::SHM);
-  conv3x3_halo_kernel<TW, BN, GN, CSF><<<grid, 512, HC::SHM, s>>>(a);
+  LS_SET_MAX_DYN_SHM((conv3x3_halo_kernel<TW, BN, GN, CSF, RP>), HC::SHM);
+  conv3x3_halo_kernel<TW, BN, GN, CSF, RP><<<grid, 512, HC::SHM, s>>>(a);
 }
 
 template <int TW, int BN>
 static void launch_halo2(const ConvArgs& a, hipStream_t s) {
   if (a.aff_scale) {
-    if (a.cs_out) launch_halo3<TW, BN, true, true>(a, s);
-    else launch_halo3<TW, BN, true, false>(a, s);
+    if (g_halo_rp) {
+      if (a.cs_out) launch_halo3<TW, BN, true, true, true>(a, s);
+      else launch_halo3<TW, BN, true, false, true>(a, s);
+    } else {
+      if (a.cs_out) launch_halo3<TW, BN, true, true>(a, s);
+      else launch_halo3<TW, BN, true, false>(a, s);
+    }
   } else {
     if (a.cs_out) launch_halo3<TW, BN, false, true>(a, s);
     else launch_halo3<TW, BN, false, false>(a, s);
@@ -2617,6 +2641,7 @@ extern "C" int ls_set_tuning(int32_t key, int32_t value) {
     case 6: g_rowblock = value != 0; return LS_OK;
     case 7: g_rowblock640 = value != 0; return LS_OK;
     case 8: g_halo = value != 0; return LS_OK;
+    case 12: g_halo_rp = value != 0; return LS_OK;
     case 9: attn_set_attn6(value != 0); return LS_OK;
     case 10: g_t256 = value; return LS_OK;
     case 11: g_rs = value; return LS_OK;

@@ -16,7 +16,9 @@ SHAPES = [  # (name, n_img, H, Cin, Cout, ksize, act)
     ("geglu1 640->5120", 16, 16, 640, 5120, 1, 1), ("ff2_1 2560->640", 16, 16, 2560, 640, 1, 0),
     ("geglu2 1280->10240", 16, 8, 1280, 10240, 1, 1), ("ff2_2 5120->1280", 16, 8, 5120, 1280, 1, 0),
     ("qkv2 1280->3840", 16, 8, 1280, 3840, 1, 0), ("plain0 320->2560", 16, 32, 320, 2560, 1, 0), ("vae conv 128 256^2", 16, 256, 128, 128, 3, 0),
-    ("vae conv 512 32^2", 16, 32, 512, 512, 3, 0),
+    ("vae conv 512 32^2", 16, 32, 512, 512, 3, 0), ("vae conv 512 64^2", 16, 64, 512, 512, 3, 0),
+    ("vae conv 256>512 64^2", 16, 64, 256, 512, 3, 0), ("vae conv 256 128^2", 16, 128, 256, 256, 3, 0),
+    ("vae conv 128>256 128^2", 16, 128, 128, 256, 3, 0),
     ("out1 640->640", 16, 16, 640, 640, 1, 0), ("out2 1280->1280", 16, 8, 1280, 1280, 1, 0),
 ]
 
@@ -97,5 +99,6 @@ if __name__ == "__main__":
         lib.ls_set_tuning(8, 0 if "nohalo" in parts else 1)
         lib.ls_set_tuning(10, 1 if "t256" in parts else 0)
         lib.ls_set_tuning(11, 1 if "rs" in parts else 0)
+        lib.ls_set_tuning(12, 1 if "hrp" in parts else 0)
         TORCH_REF = "torch" in parts
         run(arg, scale=int(sc or 1))

@@ -1,6 +1,6 @@
 """Launch one ls_conv2d shape repeatedly (PMC / trace target).
 env: SHAPE="M K N ks res" (default the 16x16-level ff2: 65536 2560 640 1 1), TILE (forced
-tile id, 0 = auto), REPS (20).  usage: python scripts/gemm_one.py"""
+tile id, 0 = auto), REPS (20), AFF=1 (GroupNorm affine on a 3x3 input).  usage: python scripts/gemm_one.py"""
 import os
 import sys
 
@@ -23,8 +23,12 @@ cin = K // (ks * ks)
 w = torch.randn(N, cin, ks, ks) / K ** 0.5
 pw = ops.Packed(pack_weight(w).to(torch.bfloat16).cuda(), torch.zeros(N, device="cuda"), cin, ks, N)
 res = torch.randn(*x.shape[:3], N, device="cuda").to(torch.bfloat16) if has_res else None
-out = ops.conv(x, pw, res=res)
+kw = {}
+if os.environ.get("AFF") and ks == 3:  # GroupNorm affine + SiLU on the input (the halo conv's GN variant)
+    kw = dict(aff=(torch.rand(x.shape[0], cin, device="cuda") + 0.5, torch.randn(x.shape[0], cin, device="cuda") * 0.1, 1, True),
+              aff_materialize=True)
+out = ops.conv(x, pw, res=res, **kw)
 for _ in range(int(os.environ.get("REPS", "20"))):
-    ops.conv(x, pw, res=res, out=out)
+    ops.conv(x, pw, res=res, out=out, **kw)
 torch.cuda.synchronize()
 print("done", M, K, N, ks, has_res)

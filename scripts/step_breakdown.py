@@ -26,11 +26,12 @@ def main():
     for n, (t, c) in sorted(agg.items(), key=lambda x: -x[1][0])[:16]:
         print(f"{t/1e6:8.3f} ms  n={c:4d} avg {t/c/1e3:7.1f}us {n}")
     agg2 = collections.defaultdict(list)
+    gemm = lambda n: 'conv_gemm' in n or 'gemm_rowblock' in n or 'conv3x3_halo' in n  # the ls_conv2d kernels
     for r in seg:
-        if 'conv_gemm' in r['Kernel_Name'] or 'gemm_rowblock' in r['Kernel_Name']:
+        if gemm(r['Kernel_Name']):
             agg2[(r['Kernel_Name'].split('(')[0].replace('void ls::conv_gemm_kernel', ''), r['Grid_Size_X'])].append(dur(r))
-    fam = [dur(r) for r in seg if 'conv_gemm' in r['Kernel_Name'] or 'gemm_rowblock' in r['Kernel_Name'] or 'splitk_reduce' in r['Kernel_Name']]
-    ncall = sum(('conv_gemm' in r['Kernel_Name'] or 'gemm_rowblock' in r['Kernel_Name']) for r in seg)
+    fam = [dur(r) for r in seg if gemm(r['Kernel_Name']) or 'splitk_reduce' in r['Kernel_Name']]
+    ncall = sum(gemm(r['Kernel_Name']) for r in seg)
     print(f"conv_gemm family: {ncall} ls_conv2d calls (+{len(fam) - ncall} split-K reduces), total {sum(fam)/1e6:.3f} ms, "
           f"avg per ls_conv2d call {sum(fam)/max(1, ncall)/1e3:.1f} us  (bench.py roofline.avg_launch_ms)")
     att = [dur(r) for r in seg if 'attn' in r['Kernel_Name']]
