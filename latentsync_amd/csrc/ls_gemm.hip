@@ -213,9 +213,9 @@ __device__ __forceinline__ int swz(int row, int ch) { return row * 8 + (ch ^ ((r
 
 // Accumulators of wave-row p -> LDS staging (fp32, pitch BN + 4).
 template <int BM, int BN, int WM, int WN>
-__device__ __forceinline__ void stage_acc(f32x4 (&acc)[BM / WM / 16][BN / WN / 16], float* st, int p) {
+__device__ __forceinline__ void stage_acc(f32x4 (&acc)[BM / WM / 16][BN / WN / 16], float* st, int p, int tid) {
   constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16, SP = BN + 4;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = tid & 63, wid = tid >> 6;
   if (wid / WN != p) return;
   const int wn = wid % WN;
 #pragma unroll
@@ -253,7 +253,7 @@ __host__ __device__ constexpr bool cs_tile_fits() {
 // (GroupNorm slots) and m0r the real first row.
 template <int BM, int BN, int WM, int WN, bool GEN, bool CSF = false, int RW = 0>
 __device__ __forceinline__ void store_tile_plain(const ConvArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
-                                                 float* st, int m0, int n0, long m0r = 0) {
+                                                 float* st, int m0, int n0, long m0r = 0, int tid_in = -1) {
   constexpr int NT = WM * WN * 64, WTM = BM / WM, SP = BN + 4;
   constexpr int CPRW = BN / 8;                 // chunk columns per tile row
   constexpr int RPI = NT / CPRW;               // rows per iteration
@@ -265,7 +265,7 @@ __device__ __forceinline__ void store_tile_plain(const ConvArgs& a, f32x4 (&acc)
     if constexpr (RW > 0) return (int)(m0r + (long)(lr / RW) * a.Wo + lr % RW);
     else return m0 + lr;
   };
-  const int tid = threadIdx.x;
+  const int tid = tid_in >= 0 ? tid_in : (int)threadIdx.x;  // (a caller in a loop passes an opaque copy)
   const int c8 = (tid % CPRW) * 8, r0 = tid / CPRW;
   const int col = n0 + c8;
   const bool cok = (r0 < RPI) && col < a.N;
@@ -287,9 +287,11 @@ __device__ __forceinline__ void store_tile_plain(const ConvArgs& a, f32x4 (&acc)
     for (int j = 0; j < 8; ++j) bb[j] += rv[j];
   }
   if (cok && a.ln_mr) load8f(a.ln_cs + col, cs);
+  // no LayerNorm fold, no per-row row vector, unit output scale: the short path
+  const bool plain = !a.ln_mr && !(a.rowvec && !rv_tile) && a.out_scale == 1.f && !(a.ablate & 8);
 #pragma unroll 1
   for (int p = 0; p < WM; ++p) {
-    stage_acc<BM, BN, WM, WN>(acc, st, p);
+    stage_acc<BM, BN, WM, WN>(acc, st, p, tid);
     float2 mr[ITER];
     uint4 rs[ITER];
 #pragma unroll
@@ -309,16 +311,25 @@ __device__ __forceinline__ void store_tile_plain(const ConvArgs& a, f32x4 (&acc)
       const float* s = st + rl * SP + c8;
       const float4 s0 = *(const float4*)s, s1 = *(const float4*)(s + 4);
       float v[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-      float r8[8], rv[8];
+      float r8[8];
       unpack8(rs[it], r8);
+      if (plain) {  // (block-uniform) bias (+ the tile's row vector) + residual: 2 VALU per value
 #pragma unroll
-      for (int j = 0; j < 8; ++j) rv[j] = 0.f;
-      if (a.rowvec && !rv_tile) load8f(a.rowvec + rv_row(a, row) + col, rv);
+        for (int j = 0; j < 8; ++j) v[j] = (v[j] + bb[j]) + r8[j];
+      } else {
+        float rv[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float x = mr[it].y * (v[j] - mr[it].x * cs[j]);
-        v[j] = (x + bb[j] + rv[j] + r8[j]) * a.out_scale;
-        if (GEN) v[j] = act_fn(a.act, v[j]);
+        for (int j = 0; j < 8; ++j) rv[j] = 0.f;
+        if (a.rowvec && !rv_tile) load8f(a.rowvec + rv_row(a, row) + col, rv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x = mr[it].y * (v[j] - mr[it].x * cs[j]);
+          v[j] = (x + bb[j] + rv[j] + r8[j]) * a.out_scale;
+        }
+      }
+      if (GEN) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = act_fn(a.act, v[j]);
       }
       if (a.ablate & 4) {
         if (v[0] == 12345.f) ((float*)a.y)[0] = v[1];
@@ -388,7 +399,7 @@ __device__ __forceinline__ void store_tile_geglu(const ConvArgs& a, f32x4 (&acc)
   if (cok && a.ln_mr) { load8f(a.ln_cs + col, ch); load8f(a.ln_cs + col + 16, cg); }
 #pragma unroll 1
   for (int p = 0; p < WM; ++p) {
-    stage_acc<BM, BN, WM, WN>(acc, st, p);
+    stage_acc<BM, BN, WM, WN>(acc, st, p, tid);
     const int rbase = m0 + p * WTM;
     float2 mr[ITER];
 #pragma unroll
@@ -1778,6 +1789,7 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
       }
     }
   };
+  const bool unit_scale = a.out_scale == 1.f;
   double S1[FM], S2[FM];  // running row sums of the output (ST), per lane: its 4-column slices
 #pragma unroll
   for (int i = 0; i < FM; ++i) { S1[i] = 0.0; S2[i] = 0.0; }
@@ -1813,8 +1825,13 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
             r4[0] = __uint_as_float(rs.x << 16); r4[1] = __uint_as_float(rs.x & 0xffff0000u);
             r4[2] = __uint_as_float(rs.y << 16); r4[3] = __uint_as_float(rs.y & 0xffff0000u);
           }
+          if (unit_scale) {  // (block-uniform)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = (acc[i][j][r] + r4[r]) * a.out_scale;
+            for (int r = 0; r < 4; ++r) o[r] = acc[i][j][r] + r4[r];
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = (acc[i][j][r] + r4[r]) * a.out_scale;
+          }
           const uint2 pk = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
           *(uint2*)(yrow + nb + 16 * j) = pk;
           if (CS) {
@@ -1988,7 +2005,7 @@ struct HaloCfg {
   static constexpr int FN = BN / 32;                     // 16-column fragments per wave
   static constexpr size_t SHM = ((size_t)2 * HALO + (size_t)NSW * WSLOT + 64 + 64) * 16;  // + dummy, affine
   static_assert(SHM <= 163840, "halo conv LDS");
-  static_assert((size_t)64 * (BN + 4) * 4 <= (size_t)2 * HALO * 16, "epilogue staging fits the halo images");
+  static_assert((size_t)64 * (BN + 4) * 4 <= (size_t)HALO * 16, "epilogue staging fits one halo image");
 };
 
 
@@ -2010,6 +2027,9 @@ __host__ __device__ constexpr int halo_issue(int t, int nhl, bool gn) {
 template <int TW, int BN, bool GN, bool CSF, bool RP = false>
 __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
   using HC = HaloCfg<TW, BN>;
+  // the patch loop only at BN 128 (the VAE's short-K convs, where a patch's prologue and
+  // epilogue weigh most): at BN 160 the loop-carried state beside 80 accumulators spills
+  constexpr bool PT = BN <= 128;
   constexpr int TH = HC::TH, P = HC::P, HALO = HC::HALO, WSLOT = HC::WSLOT, NSW = HC::NSW;
   constexpr int NPC = RP ? (TH + 2) * (TW + 2) * 8 : HALO;  // pieces per chunk
   constexpr int NHL = (NPC + 511) / 512, DPT = HC::DPT, FM = 4, FN = HC::FN, WTN = BN / 2;
@@ -2024,44 +2044,53 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
   const int wm = wid >> 1, wn = wid & 1;
   const int l16 = lane & 15, lg = lane >> 4;
   const int ntn = a.N / BN, tpr = a.W / TW, tpc = a.H / TH;
-  int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int tn = bid % ntn;
-  bid /= ntn;
-  const int txb = bid % tpr;
-  bid /= tpr;
-  const int tyb = bid % tpc;
-  const int img = bid / tpc;
-  const int y0 = tyb * TH, x0 = txb * TW, n0 = tn * BN;
+  // PERSISTENT over patches: block (tn, pb) runs the patches pb, pb + PB, ... of N tile tn
+  // (grid = ntn x PB; PB = the patch count gives one patch per block).  The chunk pipeline
+  // runs across patch boundaries: the last chunk of a patch loads / transforms / stores
+  // chunk 0 of the block's NEXT patch, and the weight ring streams its first taps, so a
+  // patch's prologue (halo load latency, weight DMA) hides under the previous patch's
+  // MFMAs; halo images, parameter slots and ring slots go by running counters.
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tn = bid % ntn, PB = gridDim.x / ntn;
+  const int npatch = a.n_img * tpr * tpc;
+  const int n0 = tn * BN;
   const long HW = (long)a.H * a.W;
   const int nchunk = a.Cin / 64;
-  const int G = 9 * nchunk;  // taps in all
+  const int G = 9 * nchunk;  // taps per patch
+  int patch = bid / ntn;
+  const int my_patches = patch < npatch ? (npatch - 1 - patch) / PB + 1 : 0;
+  if (my_patches == 0) return;
+  const int GT = my_patches * G;  // taps of this block
 
-  // ---- this thread's halo pieces: q = j*512 + tid -> pixel q / 8 = 64 j + tid / 8, logical
-  // 16-B chunk tid & 7; the swizzled slot is j*512 + hdst0 (64 j == 0 mod 8 keeps the phase)
   const int hc8 = tid & 7;
   const int hdst0 = (tid >> 3) * 8 + (hc8 ^ ((tid >> 3) & 7));
-  int hpix[NHL];  // pixel index within the image, or -1 (outside: zeros)
-  int hdst[RP ? NHL : 1];
-#pragma unroll
-  for (int j = 0; j < NHL; ++j) {
-    const int q = j * 512 + tid, hp = q >> 3;
-    if constexpr (RP) {
-      const int hr = hp / (TW + 2), hcol = hp - hr * (TW + 2);
-      const int y = y0 - 1 + hr, x = x0 - 1 + hcol;
-      const int slot = hr * P + hcol + 3;
-      hdst[j] = slot * 8 + (hc8 ^ (slot & 7));
-      hpix[j] = q < NPC && y >= 0 && y < a.H && x >= 0 && x < a.W ? y * a.W + x : -1;
-    } else {
-      const int hr = hp / P, hcol = hp - hr * P;
-      const int y = y0 - 1 + hr, x = x0 - 4 + hcol;
-      const bool ok = q < HALO && hcol >= 3 && hcol <= TW + 4 && y >= 0 && y < a.H && x >= 0 && x < a.W;
-      hpix[j] = ok ? y * a.W + x : -1;
-    }
-  }
   const uint32_t cap = 0x7FFFFFFFu;
-  const i32x4 rs1 = buffer_rsrc(a.x1 + img * HW * a.ld1, (uint32_t)min((long)HW * a.ld1 * 2, (long)cap));
-  const i32x4 rs2 = a.C2 ? buffer_rsrc(a.x2 + img * HW * a.ld2, (uint32_t)min((long)HW * a.ld2 * 2, (long)cap)) : rs1;
-  const long aff0 = (long)img * HW / a.pix_per_sample * a.Cin;
+  // per-patch geometry of the halo loads (switched to the next patch at the start of a
+  // patch's last chunk, whose halo work is the next patch's chunk 0)
+  int hpix[NHL];  // pixel index within the image, or -1 (outside: zeros)
+  i32x4 rs1, rs2;
+  long aff0;
+  auto setup = [&](int pt) {
+    const int txb = pt % tpr, tyb = (pt / tpr) % tpc, img = pt / (tpr * tpc);
+    const int y0 = tyb * TH, x0 = txb * TW;
+#pragma unroll
+    for (int j = 0; j < NHL; ++j) {
+      const int q = j * 512 + tid, hp = q >> 3;
+      if constexpr (RP) {
+        const int hr = hp / (TW + 2), hcol = hp - hr * (TW + 2);
+        const int y = y0 - 1 + hr, x = x0 - 1 + hcol;
+        hpix[j] = q < NPC && y >= 0 && y < a.H && x >= 0 && x < a.W ? y * a.W + x : -1;
+      } else {
+        const int hr = hp / P, hcol = hp - hr * P;
+        const int y = y0 - 1 + hr, x = x0 - 4 + hcol;
+        const bool ok = q < HALO && hcol >= 3 && hcol <= TW + 4 && y >= 0 && y < a.H && x >= 0 && x < a.W;
+        hpix[j] = ok ? y * a.W + x : -1;
+      }
+    }
+    rs1 = buffer_rsrc(a.x1 + img * HW * a.ld1, (uint32_t)min((long)HW * a.ld1 * 2, (long)cap));
+    rs2 = a.C2 ? buffer_rsrc(a.x2 + img * HW * a.ld2, (uint32_t)min((long)HW * a.ld2 * 2, (long)cap)) : rs1;
+    aff0 = (long)img * HW / a.pix_per_sample * a.Cin;
+  };
   uint4 hreg[HB];
   float4 gp;
   // the affine parameters of chunk ci (64 scales, 64 shifts): every thread loads one float4
@@ -2070,11 +2099,12 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
     const int k = tid & 31;
     gp = *(const float4*)((k < 16 ? a.aff_scale : a.aff_shift) + aff0 + ci * 64 + (k & 15) * 4);
   };
-  auto store_par = [&](int ci) {  // scale and shift times log2(e): store_halo applies silu_log2
+  auto store_par = [&](int par) {  // scale and shift times log2(e): store_halo applies silu_log2
     constexpr float L2E = 1.4426950408889634f;
-    if (tid < 32) gpar[(ci & 1) * 32 + tid] = make_float4(gp.x * L2E, gp.y * L2E, gp.z * L2E, gp.w * L2E);
+    if (tid < 32) gpar[par * 32 + tid] = make_float4(gp.x * L2E, gp.y * L2E, gp.z * L2E, gp.w * L2E);
   };
-  auto load_halo = [&](int ci, int b) {
+  // batch b of the halo of chunk ci (+ at b == 0 the chunk's affine parameters, when par)
+  auto load_halo = [&](int ci, int b, bool par) {
     const bool two = ci * 64 >= a.C1;
     const int ld = two ? a.ld2 : a.ld1;
     const int soff = (two ? ci * 64 - a.C1 : ci * 64) * 2;
@@ -2085,7 +2115,7 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
       hreg[j - j0] = __builtin_bit_cast(uint4, ls_raw_buffer_load_v4(two ? rs2 : rs1, vo, soff, 0));
     }
     if constexpr (GN) {
-      if (b == 0 && ci > 0) load_par(ci);
+      if (b == 0 && par) load_par(ci);
     }
   };
   auto store_halo = [&](int buf, int b) {
@@ -2112,14 +2142,18 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
           v = pack8(f);
         }
       }
-      if constexpr (RP) hb0[hdst[j]] = v;
-      else dst[j * 512] = v;
+      if constexpr (RP) {  // the piece's slot (recomputed: a register array of them spilled)
+        const int hp = (j * 512 + tid) >> 3, hr = hp / (TW + 2), slot = hp + hr * (P - TW - 2) + 3;
+        hb0[slot * 8 + (hc8 ^ (slot & 7))] = v;
+      } else {
+        dst[j * 512] = v;
+      }
     }
   };
 
-  // ---- weight DMA: tap g = 9 ci + t is K-tile g of the channel-chunk-major packing
-  // (buffer-descriptor DMA from column n0: per thread one byte offset, per tap the uniform
-  // soffset g * 128 -- no 64-bit address arithmetic in the tap loop)
+  // ---- weight DMA: running tap u (over the block's patches) is K-tile u % G of the
+  // channel-chunk-major packing (buffer descriptor from column n0: per thread one byte
+  // offset, per tap the uniform soffset -- no 64-bit address arithmetic in the tap loop)
   const i32x4 rs_w = buffer_rsrc(a.w + (long)n0 * a.K, (uint32_t)min((long)BN * a.K * 2, (long)cap));
   int wvo[DPT];
 #pragma unroll
@@ -2128,28 +2162,24 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
     const int lc = pc ^ ((row >> 1) & 7);
     wvo[j] = ((q < WSLOT ? row : 0) * a.K + lc * 8) * 2;
   }
-  auto issue_w = [&](int g) {
-    uint4* slot = wbuf + (g % NSW) * WSLOT;
+  auto issue_w = [&](int u) {
+    uint4* slot = wbuf + (u % NSW) * WSLOT;
+    const int kt = u % G;
 #pragma unroll
     for (int j = 0; j < DPT; ++j) {
       const bool live = j * 512 + wid * 64 < WSLOT;  // wave-uniform
       ls_raw_buffer_load_lds(rs_w, (__attribute__((address_space(3))) void*)(live ? slot + j * 512 + wid * 64 : dummy), 16,
-                             wvo[j], g * 128, 0, 0);
+                             wvo[j], kt * 128, 0, 0);
     }
   };
 
-  // ---- A fragment addressing: output pixel p = 64 wm + 16 i + l16 of the patch
-  const int p0 = 64 * wm + l16;
-  const int hp0 = (p0 / TW) * P + (p0 % TW) + 3;  // halo pixel of fragment 0 at tap (0, 0)
+  // ---- A fragment addressing (in tap()): output pixel p = 64 wm + 16 i + l16 of the patch
 
   f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  // prologue: weights of taps 0 .. NSW - 2, halo of chunk 0
-  for (int g = 0; g < NSW - 1 && g < G; ++g) issue_w(g);
+  // prologue: weights of taps 0 .. NSW - 2, halo of the first patch's chunk 0 (image 0)
+  setup(patch);
+  for (int u = 0; u < NSW - 1 && u < GT; ++u) issue_w(u);
   if constexpr (GN) {
     load_par(0);
     store_par(0);
@@ -2157,31 +2187,39 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
   }
 #pragma unroll
   for (int b = 0; b < 3; ++b) {
-    load_halo(0, b);
+    load_halo(0, b, false);
     store_halo(0, b);  // (the compiler waits for the loads)
   }
 
-  auto tap = [&](int ci, auto t_tag, auto last_tag) {
+  // tap t of the block's running chunk rc (chunk ci of the current patch); NX: a next chunk
+  // exists (this patch's ci + 1, or the next patch's chunk 0 -- setup() already switched)
+  auto tap = [&](int rc, int ci, auto t_tag, auto nx_tag, int tl) {
     constexpr int t = decltype(t_tag)::value;
-    constexpr bool LAST = decltype(last_tag)::value;  // no next chunk
-    const int g = 9 * ci + t;
-    // the weight DMA of tap g landed: VMEM instructions younger than it are the weights
+    // fragment addressing from tl (the chunk's opaque copy of tid: derived per chunk, these
+    // registers are not held across the patch epilogue, where the accumulators peak)
+    const int l16 = tl & 15, lg = (tl >> 4) & 3;
+    const int hp0 = ((64 * wm + l16) / TW) * P + ((64 * wm + l16) % TW) + 3;  // fragment 0, tap (0, 0)
+    constexpr bool NX = decltype(nx_tag)::value;
+    const int u = 9 * rc + t;
+    // the weight DMA of tap u landed: VMEM instructions younger than it are the weights
     // of the NSW - 2 later taps and the halo batches issued at taps t - NSW + 1 .. t - 1
-    constexpr int HY = LAST ? 0 : (t - 1 >= 0 ? halo_issue(t - 1, NHL, GN) : 0) +
-                                  (NSW >= 3 && t - 2 >= 0 ? halo_issue(t - 2, NHL, GN) : 0);
-    if (g + NSW - 2 >= G) wait_vm<0>();  // the ring's tail
+    // (younger still: a patch epilogue's loads / stores -- waiting past them is only early)
+    constexpr int HY = !NX ? 0 : (t - 1 >= 0 ? halo_issue(t - 1, NHL, GN) : 0) +
+                                 (NSW >= 3 && t - 2 >= 0 ? halo_issue(t - 2, NHL, GN) : 0);
+    if (u + NSW - 2 >= GT) wait_vm<0>();  // the ring's tail
     else wait_vm<(NSW - 2) * DPT + HY>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (g + NSW - 1 < G) issue_w(g + NSW - 1);
-    if constexpr (!LAST) {
-      if constexpr (GN && t == 1) store_par(ci + 1);  // read at taps 3 / 6 / 8, past a barrier
-      if constexpr (t == 3 || t == 6) store_halo((ci + 1) & 1, t / 3 - 1);
-      if constexpr (t == 0 || t == 3 || t == 6) load_halo(ci + 1, t / 3);
+    if (u + NSW - 1 < GT) issue_w(u + NSW - 1);
+    if constexpr (NX) {
+      const int cn = ci + 1 < nchunk ? ci + 1 : 0;  // the next chunk's index in its patch
+      if constexpr (GN && t == 1) store_par((rc + 1) & 1);  // read at taps 3 / 6 / 8, past a barrier
+      if constexpr (t == 3 || t == 6) store_halo((rc + 1) & 1, t / 3 - 1);
+      if constexpr (t == 0 || t == 3 || t == 6) load_halo(cn, t / 3, true);
     }
-    const uint4* hb = hbuf + (ci & 1) * HALO;
-    const uint4* wb = wbuf + (g % NSW) * WSLOT;
+    const uint4* hb = hbuf + (rc & 1) * HALO;
+    const uint4* wb = wbuf + (u % NSW) * WSLOT;
     constexpr int kh = t / 3, kw = t % 3;
     const int hpt = hp0 + kh * P + kw;
     const int sw = hpt & 7;
@@ -2201,27 +2239,44 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if constexpr (!LAST && t == 8) store_halo((ci + 1) & 1, 2);
+    if constexpr (NX && t == 8) store_halo((rc + 1) & 1, 2);
   };
   using I0 = std::integral_constant<int, 0>; using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>; using I3 = std::integral_constant<int, 3>;
   using I4 = std::integral_constant<int, 4>; using I5 = std::integral_constant<int, 5>;
   using I6 = std::integral_constant<int, 6>; using I7 = std::integral_constant<int, 7>;
   using I8 = std::integral_constant<int, 8>;
-  auto chunk = [&](int ci, auto last) {
-    tap(ci, I0{}, last); tap(ci, I1{}, last); tap(ci, I2{}, last);
-    tap(ci, I3{}, last); tap(ci, I4{}, last); tap(ci, I5{}, last);
-    tap(ci, I6{}, last); tap(ci, I7{}, last); tap(ci, I8{}, last);
+  auto chunk = [&](int rc, int ci, auto nx) {
+    int tl = lane;
+    asm volatile("v_mov_b32 %0, %0" : "+v"(tl));
+    tap(rc, ci, I0{}, nx, tl); tap(rc, ci, I1{}, nx, tl); tap(rc, ci, I2{}, nx, tl);
+    tap(rc, ci, I3{}, nx, tl); tap(rc, ci, I4{}, nx, tl); tap(rc, ci, I5{}, nx, tl);
+    tap(rc, ci, I6{}, nx, tl); tap(rc, ci, I7{}, nx, tl); tap(rc, ci, I8{}, nx, tl);
   };
-  for (int ci = 0; ci + 1 < nchunk; ++ci) chunk(ci, std::false_type{});
-  chunk(nchunk - 1, std::true_type{});
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  // epilogue: virtual rows (GroupNorm slots) = the patch's index within its image x 256
-  const int m0v = (int)(img * HW) + (tyb * tpr + txb) * 256;
-  const long m0r = img * HW + (long)y0 * a.W + x0;
-  store_tile_plain<256, BN, 4, 2, false, CSF, TW>(a, acc, (float*)lds_dyn, m0v, n0, m0r);
+  int rc = 0;  // running chunk of the block
+  for (int k = 0; k < (PT ? my_patches : 1); ++k, patch += PB) {
+    const int txb = patch % tpr, tyb = (patch / tpr) % tpc, img = patch / (tpr * tpc);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int ci = 0; ci + 1 < nchunk; ++ci, ++rc) chunk(rc, ci, std::true_type{});
+    if (PT && k + 1 < my_patches) {
+      setup(patch + PB);  // the last chunk's halo work is the next patch's chunk 0
+      chunk(rc, nchunk - 1, std::true_type{});
+    } else {
+      chunk(rc, nchunk - 1, std::false_type{});
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // epilogue: virtual rows (GroupNorm slots) = the patch's index within its image x 256;
+    // staged in the halo image the last chunk read (the other one holds the next chunk)
+    const int m0v = (int)(img * HW) + (tyb * tpr + txb) * 256;
+    const long m0r = img * HW + (long)(tyb * TH) * a.W + txb * TW;
+    store_tile_plain<256, BN, 4, 2, false, CSF, TW>(a, acc, (float*)(hbuf + (rc & 1) * HALO), m0v, n0, m0r);
+    ++rc;
+  }
 }
 
 // ---------------------------------------------------------------- host side
@@ -2229,7 +2284,10 @@ static bool g_force_regstage = getenv("LS_GEMM_REGSTAGE") != nullptr;
 // A/B switch: 3x3 weights packed tap-major (packing.py reads the same variable)
 static const bool g_w3_tapmajor = getenv("LS_W3_TAPMAJOR") != nullptr;
 static const int g_gemm_gm = getenv("LS_GEMM_GM") ? atoi(getenv("LS_GEMM_GM")) : 0;  // A/B switch: tile raster
-static int g_force_tile = 0, g_force_split = 0, g_ablate = 0, g_bk = 64;
+static int g_force_tile = 0, g_force_split = 0, g_bk = 64;
+// ablation bits (diagnostics; tuning key 4 or LS_GEMM_ABLATE): 1 no MFMA, 2 no operand DMA,
+// 4 no output store, 8 the general epilogue arithmetic even where the short path applies
+static int g_ablate = getenv("LS_GEMM_ABLATE") ? atoi(getenv("LS_GEMM_ABLATE")) : 0;
 
 struct TileCfg { int bm, bn, split; };
 
@@ -2494,7 +2552,24 @@ static void launch_cfg(const ConvArgs& a, int ks, bool tapu, int grid, hipStream
 
 // ---- halo-tile 3x3 conv dispatch (conv3x3_halo_kernel)
 static bool g_halo = getenv("LS_HALO") == nullptr || atoi(getenv("LS_HALO")) != 0;  // A/B switch: LS_HALO=0
-static bool g_halo_rp = getenv("LS_HALO_RP") != nullptr;  // A/B switch: halo pieces over the read pixels only
+// halo pieces over the read pixels only (default since r04k: step -0.5 ms, VAE encode
+// 503 -> 490 ms, decode 529 -> 518 ms per 48-window batch); LS_HALO_RP=0: the padded image
+static bool g_halo_rp = getenv("LS_HALO_RP") == nullptr || atoi(getenv("LS_HALO_RP")) != 0;
+// persistent halo grid (one block per CU walking its patches; LS_HALO_PT=0: one block per patch)
+static bool g_halo_pt = getenv("LS_HALO_PT") == nullptr || atoi(getenv("LS_HALO_PT")) != 0;
+
+static int device_cus() {  // compute units of the current device (cached per device)
+  static int cus[64] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) return 256;
+  if (!cus[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
 
 // patch width of the halo conv for this call (0: not taken)
 static int halo_tw(const ls_conv_desc* d, const ConvArgs& a) {
@@ -2521,7 +2596,10 @@ static int halo_tw(const ls_conv_desc* d, const ConvArgs& a) {
 template <int TW, int BN, bool GN, bool CSF, bool RP = false>
 static void launch_halo3(const ConvArgs& a, hipStream_t s) {
   using HC = HaloCfg<TW, BN>;
-  const int grid = a.n_img * (a.H / HC::TH) * (a.W / TW) * (a.N / BN);
+  const int ntn = a.N / BN, npatch = a.n_img * (a.H / HC::TH) * (a.W / TW);
+  // persistent: ntn x PB blocks, PB = the CUs per N tile (one 160-KB block per CU)
+  const int pb = g_halo_pt && BN <= 128 ? std::max(1, std::min(npatch, device_cus() / ntn)) : npatch;
+  const int grid = ntn * pb;
   LS_SET_MAX_DYN_SHM((conv3x3_halo_kernel<TW, BN, GN, CSF, RP>), HC::SHM);
   conv3x3_halo_kernel<TW, BN, GN, CSF, RP><<<grid, 512, HC::SHM, s>>>(a);
 }
@@ -2642,6 +2720,7 @@ extern "C" int ls_set_tuning(int32_t key, int32_t value) {
     case 7: g_rowblock640 = value != 0; return LS_OK;
     case 8: g_halo = value != 0; return LS_OK;
     case 12: g_halo_rp = value != 0; return LS_OK;
+    case 13: g_halo_pt = value != 0; return LS_OK;
     case 9: attn_set_attn6(value != 0); return LS_OK;
     case 10: g_t256 = value; return LS_OK;
     case 11: g_rs = value; return LS_OK;

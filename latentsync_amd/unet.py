@@ -37,8 +37,10 @@ from .weights import fill_state_dict
 _FUSED_TEMPORAL = os.environ.get("LS_FUSED_TEMPORAL", "1") != "0"
 # LS_FUSED_FF=0: the FeedForward as GEGLU row-block GEMM + W2 GEMM (A/B switch)
 _FUSED_FF = os.environ.get("LS_FUSED_FF", "1") != "0"
-# LS_FUSED_XATTN=0: the audio cross attention as q GEMM + ls_attention + out GEMM (A/B switch)
-_FUSED_XATTN = os.environ.get("LS_FUSED_XATTN", "1") != "0"
+# LS_FUSED_XATTN=1: the audio cross-attention branch at C = 320 as ONE ls_cross_attention_block
+# launch instead of q GEMM + ls_attention + out GEMM.  Off by default: measured 1-2 ms per
+# 48-window step SLOWER than the three launches (profiles/r04k_step_ab.txt)
+_FUSED_XATTN = os.environ.get("LS_FUSED_XATTN", "0") == "1"
 
 
 def _ff(h, st, ff1, ff2, ff2p):
