@@ -557,7 +557,7 @@ def worker(args):
         "window_mfma_frac": round(tf_per_frame * value / world / PEAK_BF16_TF, 4),
         "roofline": {"bound": "mfma",
                      "kernel": "conv_gemm family: every ls_conv2d call of one UNet fwd (conv_gemm_* tiled / "
-                               "gemm_rowblock GEMM + split-K reduce)",
+                               "gemm_rowblock / conv3x3_halo GEMM + split-K reduce; one launch per call)",
                      "achieved": round(probe["tflops"], 2), "peak": PEAK_BF16_TF, "unit": "TFLOP/s",
                      "frac": round(probe["tflops"] / PEAK_BF16_TF, 4), "traffic": traffic_per_call(),
                      "traffic_unit": "HBM bytes per ls_conv2d call (rocprofv3 PMC, profiles/pmc_traffic.json)",

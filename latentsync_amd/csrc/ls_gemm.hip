@@ -939,10 +939,21 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_gemm_dma_kernel(ConvArgs a)
 #pragma unroll
   for (int t = 0; t < NST - 1; ++t)
     if (kt0 + t < kt1 && do_dma) issue(kt0 + t, t);
+  // ILV (2-stage buffer-descriptor path): the next K-tile's DMA is issued after this
+  // K-tile's barrier, its wave-instructions spread between the MFMAs (sched_group_barrier)
+  // instead of one burst before the wait -- an LDS-DMA instruction costs ~60 issue cycles
+  // among MFMAs but 100-185 in a burst beside the fragment reads (MI355X_MICROARCH.md).  Its
+  // stage was last read in K-tile kt - 1, whose trailing barrier every wave has passed.
+  constexpr bool ILV = false;  // (A/B: BUF && NST == 2)
+  constexpr bool ILV_SGB = false;  // explicit interleave (sched_group_barrier): see DESIGN
   int stage = 0;
-  for (int kt = kt0; kt < kt1; ++kt) {
-    if (kt + NST - 1 < kt1 && do_dma) issue(kt + NST - 1, (stage + NST - 1) % NST);
-    const int ahead = min(NST - 1, kt1 - 1 - kt);
+  // one K-tile; IS: issue the next K-tile's DMA inside it (ILV).  (Peeling the last K-tile so
+  // that the DMA and the MFMAs share one basic block made the register allocator rotate the
+  // accumulators through AGPR moves, ~90 per K-tile: not kept.)
+  auto ktile = [&](int kt, auto is_tag) {
+    constexpr bool IS = decltype(is_tag)::value;
+    if (!ILV && kt + NST - 1 < kt1 && do_dma) issue(kt + NST - 1, (stage + NST - 1) % NST);
+    const int ahead = ILV ? 0 : min(NST - 1, kt1 - 1 - kt);
     if (NST >= 4 && ahead >= 3) wait_vm<3 * L>();
     else if (NST >= 3 && ahead >= 2) wait_vm<2 * L>();
     else if (ahead >= 1) wait_vm<L>();
@@ -961,6 +972,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_gemm_dma_kernel(ConvArgs a)
       for (int j = 0; j < FN; ++j)
         bfr[ks][j] = __builtin_bit_cast(bf16x8, cur[BM * CPR + swz_bk<BK>(wn * WTN + j * 16 + (lane & 15), c)]);
     }
+    if (ILV && IS && kt + 1 < kt1 && do_dma) issue(kt + 1, stage ^ 1);
 #ifdef LS_GEMM_ABLATE
     if (!(a.ablate & 16))
 #endif
@@ -973,6 +985,16 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_gemm_dma_kernel(ConvArgs a)
           for (int j = 0; j < FN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bfr[ks][j], acc[i][j], 0, 0, 0);
     }
+    if constexpr (ILV && IS && ILV_SGB) {  // fragment reads first, then L x (one DMA, MFMAs), the rest
+      constexpr int NMF = KSTEPS * FM * FN, PER = NMF / (L + 1) > 0 ? NMF / (L + 1) : 1;
+      __builtin_amdgcn_sched_group_barrier(0x100, KSTEPS * (FM + FN), 0);
+#pragma unroll
+      for (int r = 0; r < L; ++r) {
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, PER, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, NMF - L * PER > 0 ? NMF - L * PER : 0, 0);
+    }
 #ifdef LS_GEMM_ABLATE
     else if (a.ablate & 32) {
       acc[0][0][0] += (float)af[0][0][0] + (float)bfr[0][0][0];
@@ -982,7 +1004,8 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_gemm_dma_kernel(ConvArgs a)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     stage = stage + 1 == NST ? 0 : stage + 1;
-  }
+  };
+  for (int kt = kt0; kt < kt1; ++kt) ktile(kt, std::true_type{});
 #ifdef LS_GEMM_ABLATE  // diagnostic build only (hipcc -DLS_GEMM_ABLATE): it costs registers
   if (a.ablate & 8) {  // tuning: no epilogue at all (keep the accumulators live)
     float t = 0.f;
@@ -2027,9 +2050,6 @@ __host__ __device__ constexpr int halo_issue(int t, int nhl, bool gn) {
 template <int TW, int BN, bool GN, bool CSF, bool RP = false>
 __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
   using HC = HaloCfg<TW, BN>;
-  // the patch loop only at BN 128 (the VAE's short-K convs, where a patch's prologue and
-  // epilogue weigh most): at BN 160 the loop-carried state beside 80 accumulators spills
-  constexpr bool PT = BN <= 128;
   constexpr int TH = HC::TH, P = HC::P, HALO = HC::HALO, WSLOT = HC::WSLOT, NSW = HC::NSW;
   constexpr int NPC = RP ? (TH + 2) * (TW + 2) * 8 : HALO;  // pieces per chunk
   constexpr int NHL = (NPC + 511) / 512, DPT = HC::DPT, FM = 4, FN = HC::FN, WTN = BN / 2;
@@ -2044,53 +2064,44 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
   const int wm = wid >> 1, wn = wid & 1;
   const int l16 = lane & 15, lg = lane >> 4;
   const int ntn = a.N / BN, tpr = a.W / TW, tpc = a.H / TH;
-  // PERSISTENT over patches: block (tn, pb) runs the patches pb, pb + PB, ... of N tile tn
-  // (grid = ntn x PB; PB = the patch count gives one patch per block).  The chunk pipeline
-  // runs across patch boundaries: the last chunk of a patch loads / transforms / stores
-  // chunk 0 of the block's NEXT patch, and the weight ring streams its first taps, so a
-  // patch's prologue (halo load latency, weight DMA) hides under the previous patch's
-  // MFMAs; halo images, parameter slots and ring slots go by running counters.
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int tn = bid % ntn, PB = gridDim.x / ntn;
-  const int npatch = a.n_img * tpr * tpc;
-  const int n0 = tn * BN;
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tn = bid % ntn;
+  bid /= ntn;
+  const int txb = bid % tpr;
+  bid /= tpr;
+  const int tyb = bid % tpc;
+  const int img = bid / tpc;
+  const int y0 = tyb * TH, x0 = txb * TW, n0 = tn * BN;
   const long HW = (long)a.H * a.W;
   const int nchunk = a.Cin / 64;
-  const int G = 9 * nchunk;  // taps per patch
-  int patch = bid / ntn;
-  const int my_patches = patch < npatch ? (npatch - 1 - patch) / PB + 1 : 0;
-  if (my_patches == 0) return;
-  const int GT = my_patches * G;  // taps of this block
+  const int G = 9 * nchunk;  // taps in all
 
+  // ---- this thread's halo pieces: q = j*512 + tid -> pixel q / 8 = 64 j + tid / 8, logical
+  // 16-B chunk tid & 7; the swizzled slot is j*512 + hdst0 (64 j == 0 mod 8 keeps the phase)
   const int hc8 = tid & 7;
   const int hdst0 = (tid >> 3) * 8 + (hc8 ^ ((tid >> 3) & 7));
-  const uint32_t cap = 0x7FFFFFFFu;
-  // per-patch geometry of the halo loads (switched to the next patch at the start of a
-  // patch's last chunk, whose halo work is the next patch's chunk 0)
   int hpix[NHL];  // pixel index within the image, or -1 (outside: zeros)
-  i32x4 rs1, rs2;
-  long aff0;
-  auto setup = [&](int pt) {
-    const int txb = pt % tpr, tyb = (pt / tpr) % tpc, img = pt / (tpr * tpc);
-    const int y0 = tyb * TH, x0 = txb * TW;
+  int hdst[RP ? NHL : 1];
 #pragma unroll
-    for (int j = 0; j < NHL; ++j) {
-      const int q = j * 512 + tid, hp = q >> 3;
-      if constexpr (RP) {
-        const int hr = hp / (TW + 2), hcol = hp - hr * (TW + 2);
-        const int y = y0 - 1 + hr, x = x0 - 1 + hcol;
-        hpix[j] = q < NPC && y >= 0 && y < a.H && x >= 0 && x < a.W ? y * a.W + x : -1;
-      } else {
-        const int hr = hp / P, hcol = hp - hr * P;
-        const int y = y0 - 1 + hr, x = x0 - 4 + hcol;
-        const bool ok = q < HALO && hcol >= 3 && hcol <= TW + 4 && y >= 0 && y < a.H && x >= 0 && x < a.W;
-        hpix[j] = ok ? y * a.W + x : -1;
-      }
+  for (int j = 0; j < NHL; ++j) {
+    const int q = j * 512 + tid, hp = q >> 3;
+    if constexpr (RP) {
+      const int hr = hp / (TW + 2), hcol = hp - hr * (TW + 2);
+      const int y = y0 - 1 + hr, x = x0 - 1 + hcol;
+      const int slot = hr * P + hcol + 3;
+      hdst[j] = slot * 8 + (hc8 ^ (slot & 7));
+      hpix[j] = q < NPC && y >= 0 && y < a.H && x >= 0 && x < a.W ? y * a.W + x : -1;
+    } else {
+      const int hr = hp / P, hcol = hp - hr * P;
+      const int y = y0 - 1 + hr, x = x0 - 4 + hcol;
+      const bool ok = q < HALO && hcol >= 3 && hcol <= TW + 4 && y >= 0 && y < a.H && x >= 0 && x < a.W;
+      hpix[j] = ok ? y * a.W + x : -1;
     }
-    rs1 = buffer_rsrc(a.x1 + img * HW * a.ld1, (uint32_t)min((long)HW * a.ld1 * 2, (long)cap));
-    rs2 = a.C2 ? buffer_rsrc(a.x2 + img * HW * a.ld2, (uint32_t)min((long)HW * a.ld2 * 2, (long)cap)) : rs1;
-    aff0 = (long)img * HW / a.pix_per_sample * a.Cin;
-  };
+  }
+  const uint32_t cap = 0x7FFFFFFFu;
+  const i32x4 rs1 = buffer_rsrc(a.x1 + img * HW * a.ld1, (uint32_t)min((long)HW * a.ld1 * 2, (long)cap));
+  const i32x4 rs2 = a.C2 ? buffer_rsrc(a.x2 + img * HW * a.ld2, (uint32_t)min((long)HW * a.ld2 * 2, (long)cap)) : rs1;
+  const long aff0 = (long)img * HW / a.pix_per_sample * a.Cin;
   uint4 hreg[HB];
   float4 gp;
   // the affine parameters of chunk ci (64 scales, 64 shifts): every thread loads one float4
@@ -2099,12 +2110,11 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
     const int k = tid & 31;
     gp = *(const float4*)((k < 16 ? a.aff_scale : a.aff_shift) + aff0 + ci * 64 + (k & 15) * 4);
   };
-  auto store_par = [&](int par) {  // scale and shift times log2(e): store_halo applies silu_log2
+  auto store_par = [&](int ci) {  // scale and shift times log2(e): store_halo applies silu_log2
     constexpr float L2E = 1.4426950408889634f;
-    if (tid < 32) gpar[par * 32 + tid] = make_float4(gp.x * L2E, gp.y * L2E, gp.z * L2E, gp.w * L2E);
+    if (tid < 32) gpar[(ci & 1) * 32 + tid] = make_float4(gp.x * L2E, gp.y * L2E, gp.z * L2E, gp.w * L2E);
   };
-  // batch b of the halo of chunk ci (+ at b == 0 the chunk's affine parameters, when par)
-  auto load_halo = [&](int ci, int b, bool par) {
+  auto load_halo = [&](int ci, int b) {
     const bool two = ci * 64 >= a.C1;
     const int ld = two ? a.ld2 : a.ld1;
     const int soff = (two ? ci * 64 - a.C1 : ci * 64) * 2;
@@ -2115,7 +2125,7 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
       hreg[j - j0] = __builtin_bit_cast(uint4, ls_raw_buffer_load_v4(two ? rs2 : rs1, vo, soff, 0));
     }
     if constexpr (GN) {
-      if (b == 0 && par) load_par(ci);
+      if (b == 0 && ci > 0) load_par(ci);
     }
   };
   auto store_halo = [&](int buf, int b) {
@@ -2142,18 +2152,14 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
           v = pack8(f);
         }
       }
-      if constexpr (RP) {  // the piece's slot (recomputed: a register array of them spilled)
-        const int hp = (j * 512 + tid) >> 3, hr = hp / (TW + 2), slot = hp + hr * (P - TW - 2) + 3;
-        hb0[slot * 8 + (hc8 ^ (slot & 7))] = v;
-      } else {
-        dst[j * 512] = v;
-      }
+      if constexpr (RP) hb0[hdst[j]] = v;
+      else dst[j * 512] = v;
     }
   };
 
-  // ---- weight DMA: running tap u (over the block's patches) is K-tile u % G of the
-  // channel-chunk-major packing (buffer descriptor from column n0: per thread one byte
-  // offset, per tap the uniform soffset -- no 64-bit address arithmetic in the tap loop)
+  // ---- weight DMA: tap g = 9 ci + t is K-tile g of the channel-chunk-major packing
+  // (buffer-descriptor DMA from column n0: per thread one byte offset, per tap the uniform
+  // soffset g * 128 -- no 64-bit address arithmetic in the tap loop)
   const i32x4 rs_w = buffer_rsrc(a.w + (long)n0 * a.K, (uint32_t)min((long)BN * a.K * 2, (long)cap));
   int wvo[DPT];
 #pragma unroll
@@ -2162,24 +2168,28 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
     const int lc = pc ^ ((row >> 1) & 7);
     wvo[j] = ((q < WSLOT ? row : 0) * a.K + lc * 8) * 2;
   }
-  auto issue_w = [&](int u) {
-    uint4* slot = wbuf + (u % NSW) * WSLOT;
-    const int kt = u % G;
+  auto issue_w = [&](int g) {
+    uint4* slot = wbuf + (g % NSW) * WSLOT;
 #pragma unroll
     for (int j = 0; j < DPT; ++j) {
       const bool live = j * 512 + wid * 64 < WSLOT;  // wave-uniform
       ls_raw_buffer_load_lds(rs_w, (__attribute__((address_space(3))) void*)(live ? slot + j * 512 + wid * 64 : dummy), 16,
-                             wvo[j], kt * 128, 0, 0);
+                             wvo[j], g * 128, 0, 0);
     }
   };
 
-  // ---- A fragment addressing (in tap()): output pixel p = 64 wm + 16 i + l16 of the patch
+  // ---- A fragment addressing: output pixel p = 64 wm + 16 i + l16 of the patch
+  const int p0 = 64 * wm + l16;
+  const int hp0 = (p0 / TW) * P + (p0 % TW) + 3;  // halo pixel of fragment 0 at tap (0, 0)
 
   f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  // prologue: weights of taps 0 .. NSW - 2, halo of the first patch's chunk 0 (image 0)
-  setup(patch);
-  for (int u = 0; u < NSW - 1 && u < GT; ++u) issue_w(u);
+  // prologue: weights of taps 0 .. NSW - 2, halo of chunk 0
+  for (int g = 0; g < NSW - 1 && g < G; ++g) issue_w(g);
   if constexpr (GN) {
     load_par(0);
     store_par(0);
@@ -2187,39 +2197,31 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
   }
 #pragma unroll
   for (int b = 0; b < 3; ++b) {
-    load_halo(0, b, false);
+    load_halo(0, b);
     store_halo(0, b);  // (the compiler waits for the loads)
   }
 
-  // tap t of the block's running chunk rc (chunk ci of the current patch); NX: a next chunk
-  // exists (this patch's ci + 1, or the next patch's chunk 0 -- setup() already switched)
-  auto tap = [&](int rc, int ci, auto t_tag, auto nx_tag, int tl) {
+  auto tap = [&](int ci, auto t_tag, auto last_tag) {
     constexpr int t = decltype(t_tag)::value;
-    // fragment addressing from tl (the chunk's opaque copy of tid: derived per chunk, these
-    // registers are not held across the patch epilogue, where the accumulators peak)
-    const int l16 = tl & 15, lg = (tl >> 4) & 3;
-    const int hp0 = ((64 * wm + l16) / TW) * P + ((64 * wm + l16) % TW) + 3;  // fragment 0, tap (0, 0)
-    constexpr bool NX = decltype(nx_tag)::value;
-    const int u = 9 * rc + t;
-    // the weight DMA of tap u landed: VMEM instructions younger than it are the weights
+    constexpr bool LAST = decltype(last_tag)::value;  // no next chunk
+    const int g = 9 * ci + t;
+    // the weight DMA of tap g landed: VMEM instructions younger than it are the weights
     // of the NSW - 2 later taps and the halo batches issued at taps t - NSW + 1 .. t - 1
-    // (younger still: a patch epilogue's loads / stores -- waiting past them is only early)
-    constexpr int HY = !NX ? 0 : (t - 1 >= 0 ? halo_issue(t - 1, NHL, GN) : 0) +
-                                 (NSW >= 3 && t - 2 >= 0 ? halo_issue(t - 2, NHL, GN) : 0);
-    if (u + NSW - 2 >= GT) wait_vm<0>();  // the ring's tail
+    constexpr int HY = LAST ? 0 : (t - 1 >= 0 ? halo_issue(t - 1, NHL, GN) : 0) +
+                                  (NSW >= 3 && t - 2 >= 0 ? halo_issue(t - 2, NHL, GN) : 0);
+    if (g + NSW - 2 >= G) wait_vm<0>();  // the ring's tail
     else wait_vm<(NSW - 2) * DPT + HY>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (u + NSW - 1 < GT) issue_w(u + NSW - 1);
-    if constexpr (NX) {
-      const int cn = ci + 1 < nchunk ? ci + 1 : 0;  // the next chunk's index in its patch
-      if constexpr (GN && t == 1) store_par((rc + 1) & 1);  // read at taps 3 / 6 / 8, past a barrier
-      if constexpr (t == 3 || t == 6) store_halo((rc + 1) & 1, t / 3 - 1);
-      if constexpr (t == 0 || t == 3 || t == 6) load_halo(cn, t / 3, true);
+    if (g + NSW - 1 < G) issue_w(g + NSW - 1);
+    if constexpr (!LAST) {
+      if constexpr (GN && t == 1) store_par(ci + 1);  // read at taps 3 / 6 / 8, past a barrier
+      if constexpr (t == 3 || t == 6) store_halo((ci + 1) & 1, t / 3 - 1);
+      if constexpr (t == 0 || t == 3 || t == 6) load_halo(ci + 1, t / 3);
     }
-    const uint4* hb = hbuf + (rc & 1) * HALO;
-    const uint4* wb = wbuf + (u % NSW) * WSLOT;
+    const uint4* hb = hbuf + (ci & 1) * HALO;
+    const uint4* wb = wbuf + (g % NSW) * WSLOT;
     constexpr int kh = t / 3, kw = t % 3;
     const int hpt = hp0 + kh * P + kw;
     const int sw = hpt & 7;
@@ -2239,44 +2241,27 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if constexpr (NX && t == 8) store_halo((rc + 1) & 1, 2);
+    if constexpr (!LAST && t == 8) store_halo((ci + 1) & 1, 2);
   };
   using I0 = std::integral_constant<int, 0>; using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>; using I3 = std::integral_constant<int, 3>;
   using I4 = std::integral_constant<int, 4>; using I5 = std::integral_constant<int, 5>;
   using I6 = std::integral_constant<int, 6>; using I7 = std::integral_constant<int, 7>;
   using I8 = std::integral_constant<int, 8>;
-  auto chunk = [&](int rc, int ci, auto nx) {
-    int tl = lane;
-    asm volatile("v_mov_b32 %0, %0" : "+v"(tl));
-    tap(rc, ci, I0{}, nx, tl); tap(rc, ci, I1{}, nx, tl); tap(rc, ci, I2{}, nx, tl);
-    tap(rc, ci, I3{}, nx, tl); tap(rc, ci, I4{}, nx, tl); tap(rc, ci, I5{}, nx, tl);
-    tap(rc, ci, I6{}, nx, tl); tap(rc, ci, I7{}, nx, tl); tap(rc, ci, I8{}, nx, tl);
+  auto chunk = [&](int ci, auto last) {
+    tap(ci, I0{}, last); tap(ci, I1{}, last); tap(ci, I2{}, last);
+    tap(ci, I3{}, last); tap(ci, I4{}, last); tap(ci, I5{}, last);
+    tap(ci, I6{}, last); tap(ci, I7{}, last); tap(ci, I8{}, last);
   };
-  int rc = 0;  // running chunk of the block
-  for (int k = 0; k < (PT ? my_patches : 1); ++k, patch += PB) {
-    const int txb = patch % tpr, tyb = (patch / tpr) % tpc, img = patch / (tpr * tpc);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    for (int ci = 0; ci + 1 < nchunk; ++ci, ++rc) chunk(rc, ci, std::true_type{});
-    if (PT && k + 1 < my_patches) {
-      setup(patch + PB);  // the last chunk's halo work is the next patch's chunk 0
-      chunk(rc, nchunk - 1, std::true_type{});
-    } else {
-      chunk(rc, nchunk - 1, std::false_type{});
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    // epilogue: virtual rows (GroupNorm slots) = the patch's index within its image x 256;
-    // staged in the halo image the last chunk read (the other one holds the next chunk)
-    const int m0v = (int)(img * HW) + (tyb * tpr + txb) * 256;
-    const long m0r = img * HW + (long)(tyb * TH) * a.W + txb * TW;
-    store_tile_plain<256, BN, 4, 2, false, CSF, TW>(a, acc, (float*)(hbuf + (rc & 1) * HALO), m0v, n0, m0r);
-    ++rc;
-  }
+  for (int ci = 0; ci + 1 < nchunk; ++ci) chunk(ci, std::false_type{});
+  chunk(nchunk - 1, std::true_type{});
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  // epilogue: virtual rows (GroupNorm slots) = the patch's index within its image x 256
+  const int m0v = (int)(img * HW) + (tyb * tpr + txb) * 256;
+  const long m0r = img * HW + (long)y0 * a.W + x0;
+  store_tile_plain<256, BN, 4, 2, false, CSF, TW>(a, acc, (float*)lds_dyn, m0v, n0, m0r);
 }
 
 // ---------------------------------------------------------------- host side
@@ -2555,21 +2540,6 @@ static bool g_halo = getenv("LS_HALO") == nullptr || atoi(getenv("LS_HALO")) != 
 // halo pieces over the read pixels only (default since r04k: step -0.5 ms, VAE encode
 // 503 -> 490 ms, decode 529 -> 518 ms per 48-window batch); LS_HALO_RP=0: the padded image
 static bool g_halo_rp = getenv("LS_HALO_RP") == nullptr || atoi(getenv("LS_HALO_RP")) != 0;
-// persistent halo grid (one block per CU walking its patches; LS_HALO_PT=0: one block per patch)
-static bool g_halo_pt = getenv("LS_HALO_PT") == nullptr || atoi(getenv("LS_HALO_PT")) != 0;
-
-static int device_cus() {  // compute units of the current device (cached per device)
-  static int cus[64] = {0};
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  if (dev < 0 || dev >= 64) return 256;
-  if (!cus[dev]) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    cus[dev] = n;
-  }
-  return cus[dev];
-}
 
 // patch width of the halo conv for this call (0: not taken)
 static int halo_tw(const ls_conv_desc* d, const ConvArgs& a) {
@@ -2596,10 +2566,7 @@ static int halo_tw(const ls_conv_desc* d, const ConvArgs& a) {
 template <int TW, int BN, bool GN, bool CSF, bool RP = false>
 static void launch_halo3(const ConvArgs& a, hipStream_t s) {
   using HC = HaloCfg<TW, BN>;
-  const int ntn = a.N / BN, npatch = a.n_img * (a.H / HC::TH) * (a.W / TW);
-  // persistent: ntn x PB blocks, PB = the CUs per N tile (one 160-KB block per CU)
-  const int pb = g_halo_pt && BN <= 128 ? std::max(1, std::min(npatch, device_cus() / ntn)) : npatch;
-  const int grid = ntn * pb;
+  const int grid = a.n_img * (a.H / HC::TH) * (a.W / TW) * (a.N / BN);
   LS_SET_MAX_DYN_SHM((conv3x3_halo_kernel<TW, BN, GN, CSF, RP>), HC::SHM);
   conv3x3_halo_kernel<TW, BN, GN, CSF, RP><<<grid, 512, HC::SHM, s>>>(a);
 }
@@ -2720,7 +2687,6 @@ extern "C" int ls_set_tuning(int32_t key, int32_t value) {
     case 7: g_rowblock640 = value != 0; return LS_OK;
     case 8: g_halo = value != 0; return LS_OK;
     case 12: g_halo_rp = value != 0; return LS_OK;
-    case 13: g_halo_pt = value != 0; return LS_OK;
     case 9: attn_set_attn6(value != 0); return LS_OK;
     case 10: g_t256 = value; return LS_OK;
     case 11: g_rs = value; return LS_OK;

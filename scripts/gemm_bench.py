@@ -100,6 +100,5 @@ if __name__ == "__main__":
         lib.ls_set_tuning(10, 1 if "t256" in parts else 0)
         lib.ls_set_tuning(11, 1 if "rs" in parts else 0)
         lib.ls_set_tuning(12, 0 if "nohrp" in parts else 1)
-        lib.ls_set_tuning(13, 0 if "nopt" in parts else 1)
         TORCH_REF = "torch" in parts
         run(arg, scale=int(sc or 1))

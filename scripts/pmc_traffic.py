@@ -41,8 +41,9 @@ def one_step(disp):
 
 
 def family(seg):
-    calls = sum(("conv_gemm" in n or "gemm_rowblock" in n) for _, n, _ in seg)
-    kib = sum(v for _, n, v in seg if "conv_gemm" in n or "gemm_rowblock" in n or "splitk_reduce" in n)
+    fam = lambda n: "conv_gemm" in n or "gemm_rowblock" in n or "conv3x3_halo" in n  # the ls_conv2d kernels
+    calls = sum(fam(n) for _, n, _ in seg)
+    kib = sum(v for _, n, v in seg if fam(n) or "splitk_reduce" in n)
     return calls, kib
 
 
@@ -56,7 +57,7 @@ def main():
     attn_f = [v for _, n, v in fetch if "attn" in n]
     attn_w = [v for _, n, v in write if "attn" in n]
     res = {
-        "kernel": "conv_gemm family (every ls_conv2d call: tiled / row-block GEMM + split-K reduce), one UNet step",
+        "kernel": "conv_gemm family (every ls_conv2d call: tiled / row-block / halo-tile GEMM + split-K reduce), one UNet step",
         "calls": cf,
         "fetch_bytes_per_call": fb, "write_bytes_per_call": wb, "hbm_bytes_per_call": fb + wb,
         "fetch_raw_kib_step": fk, "write_kib_step": wk,
