@@ -2543,6 +2543,10 @@ static bool g_halo = getenv("LS_HALO") == nullptr || atoi(getenv("LS_HALO")) != 
 // 503 -> 490 ms, decode 529 -> 518 ms per 48-window batch); LS_HALO_RP=0: the padded image
 static bool g_halo_rp = getenv("LS_HALO_RP") == nullptr || atoi(getenv("LS_HALO_RP")) != 0;
 
+// A/B switch (tuning key 13): 128-channel tiles where both divide N (3-slot weight ring
+// instead of 2 at BN 160)
+static bool g_halo_bn128 = getenv("LS_HALO_BN128") != nullptr;
+
 // patch width of the halo conv for this call (0: not taken)
 static int halo_tw(const ls_conv_desc* d, const ConvArgs& a) {
   if (!g_halo || g_force_tile || g_force_regstage || d->ksize != 3 || a.stride != 1 || a.pad != 1 || a.upsample ||
@@ -2591,7 +2595,7 @@ static void launch_halo2(const ConvArgs& a, hipStream_t s) {
 
 template <int TW>
 static void launch_halo1(const ConvArgs& a, hipStream_t s) {
-  if (a.N % 160 == 0) launch_halo2<TW, 160>(a, s);
+  if (a.N % 160 == 0 && !(g_halo_bn128 && a.N % 128 == 0)) launch_halo2<TW, 160>(a, s);
   else launch_halo2<TW, 128>(a, s);
 }
 
@@ -2689,6 +2693,7 @@ extern "C" int ls_set_tuning(int32_t key, int32_t value) {
     case 7: g_rowblock640 = value != 0; return LS_OK;
     case 8: g_halo = value != 0; return LS_OK;
     case 12: g_halo_rp = value != 0; return LS_OK;
+    case 13: g_halo_bn128 = value != 0; return LS_OK;
     case 9: attn_set_attn6(value != 0); return LS_OK;
     case 10: g_t256 = value; return LS_OK;
     case 11: g_rs = value; return LS_OK;
