@@ -371,9 +371,13 @@ int ls_add_rows(const uint16_t* x, int64_t rows, int32_t C, int32_t ldx, const f
 /* Tuning / A-B switches for ls_conv2d (process-wide, host side only):
  * key 1 = force the register-staged kernel (1) instead of the LDS-DMA one;
  * key 2 = force tile 0 auto, 1 128x128, 2 128x64, 3 64x64, 4 128x32; key 3 = split-K with key 2;
- * key 4 = ablation (1 skip MFMA, 2 skip operand DMA; timing only); key 5 = DMA K-tile depth 32 or 64;
+ * key 4 = ablation (1 skip MFMA, 2 skip operand DMA, 4 skip the output store, 8 the general epilogue
+ * arithmetic; timing only); key 5 = DMA K-tile depth 32 or 64;
  * key 6 = row-block GEMM on / off; key 7 = its K = 640 instances on / off; key 8 = halo-tile 3x3
- * conv on / off (ABI 12); key 9 = d = 40 self attention on the 32x32x16 kernel (ABI 12). */
+ * conv on / off (ABI 12); key 9 = d = 40 self attention on the 32x32x16 kernel (ABI 12);
+ * key 10 = 256x128 3-stage tile for the short-K linears; key 11 = register-staged operand loads in
+ * the tiled GEMM; key 12 = halo pieces over the read pixels only (default on); key 13 = 128-channel
+ * halo tiles where 160 also divides N.  Keys 10, 11, 13 are measured-slower A/B options. */
 int ls_set_tuning(int32_t key, int32_t value);
 
 /* Diagnostics: workgroups per CU the runtime can co-schedule for a GEMM kernel
