@@ -2203,6 +2203,18 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
     store_halo(0, b);  // (the compiler waits for the loads)
   }
 
+  bf16x8 apf[2][FM];  // A fragments of the current tap (both k-steps)
+  auto read_a = [&](const uint4* hb, int tt) {  // (tt compile-time after inlining)
+    const int hpt = hp0 + (tt / 3) * P + tt % 3;
+    const int sw = hpt & 7;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int base = hpt * 8 + ((ks * 4 + lg) ^ sw);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)  // fragment i: + ((16 i) / TW) rows, + (16 i) % TW pixels
+        apf[ks][i] = __builtin_bit_cast(bf16x8, hb[base + 8 * (((16 * i) / TW) * P + (16 * i) % TW)]);
+    }
+  };
   auto tap = [&](int ci, auto t_tag, auto last_tag) {
     constexpr int t = decltype(t_tag)::value;
     constexpr bool LAST = decltype(last_tag)::value;  // no next chunk
@@ -2224,16 +2236,14 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
     }
     const uint4* hb = hbuf + (ci & 1) * HALO;
     const uint4* wb = wbuf + (g % NSW) * WSLOT;
-    constexpr int kh = t / 3, kw = t % 3;
-    const int hpt = hp0 + kh * P + kw;
-    const int sw = hpt & 7;
+    // A fragments of tap t: at t = 0 read here; for t > 0 read at the end of tap t - 1 (the
+    // halo image is stable within a chunk), so after this tap's barrier only the weight
+    // fragments stand between the wave and its MFMAs, and the LDS array serves 10 reads per
+    // wave there instead of 18
+    if constexpr (t == 0) read_a(hb, 0);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const int base = hpt * 8 + ((ks * 4 + lg) ^ sw);
-      bf16x8 af[FM], bfr[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i)  // fragment i: + ((16 i) / TW) rows, + (16 i) % TW pixels
-        af[i] = __builtin_bit_cast(bf16x8, hb[base + 8 * (((16 * i) / TW) * P + (16 * i) % TW)]);
+      bf16x8 bfr[FN];
 #pragma unroll
       for (int j = 0; j < FN; ++j)
         bfr[j] = __builtin_bit_cast(bf16x8, wb[swz_bk<64>(wn * WTN + j * 16 + l16, ks * 4 + lg)]);
@@ -2241,8 +2251,9 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(apf[ks][i], bfr[j], acc[i][j], 0, 0, 0);
     }
+    if constexpr (t < 8) read_a(hb, t + 1);
     if constexpr (!LAST && t == 8) store_halo((ci + 1) & 1, 2);
   };
   using I0 = std::integral_constant<int, 0>; using I1 = std::integral_constant<int, 1>;
