@@ -1122,6 +1122,122 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_gemm_rs_kernel(ConvArgs a) 
   store_tile<BM, BN, WM, WN, EPI>(a, acc, (float*)lds, m0, n0, 0);
 }
 
+// 1x1 GEMM with the A operand straight into registers (A/B switch LS_GEMM_AREG / tuning key
+// 14): a lane's A fragment of a 32-wide k-step is 8 consecutive channels of one row -- 16
+// contiguous bytes of the NHWC activation -- so it is one buffer_load_dwordx4 into the MFMA
+// operand registers, no LDS.  Only B (the weights) goes through an LDS-DMA ring (3 stages,
+// 20 KB each at BN 160): per K-tile a wave issues BN/32 LDS-DMA instructions instead of
+// (BM + BN)/32, the rest of the operand traffic being plain vector loads (each A element is
+// read by the WN waves of its row band, from L1 / L2).  A of K-tile kt + 1 is loaded during
+// K-tile kt (two register sets, the K loop unrolled by 2 so the sets are static).
+template <int BM, int BN, int WM, int WN, int EPI>
+__global__ void __launch_bounds__(WM * WN * 64) conv_gemm_areg_kernel(ConvArgs a) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  constexpr int BI = BN * 8 / NT;
+  static_assert((BN * 8) % NT == 0, "B pieces must divide over the threads");
+  constexpr int STAGE = BN * 8;  // uint4 per B stage
+  extern __shared__ __attribute__((aligned(16))) uint4 lds_dyn[];
+  uint4* lds = lds_dyn;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l16 = lane & 15, lg = lane >> 4;
+  const int wm = wid / WN, wn = wid % WN;
+  const int nt = a.ntm * a.ntn;
+  int bid = xcd_remap(blockIdx.x, nt);
+  int tm, tn;
+  tile_of(a, bid, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kt1 = a.K / 64;
+  const long cap = 0x7FFFFFFFL;
+
+  // A: rows past M read zeros (descriptor size); concat K-tiles from x2 (host: C1 % 64 == 0)
+  const i32x4 rs_a1 = buffer_rsrc(a.x1 + (long)m0 * a.ld1, (uint32_t)min((long)(a.M - m0) * a.ld1 * 2, cap));
+  const i32x4 rs_a2 =
+      a.C2 ? buffer_rsrc(a.x2 + (long)m0 * a.ld2, (uint32_t)min((long)(a.M - m0) * a.ld2 * 2, cap)) : rs_a1;
+  int avo1[FM], avo2[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int r = wm * WTM + i * 16 + l16;
+    avo1[i] = (r * a.ld1 + lg * 8) * 2;
+    avo2[i] = (r * a.ld2 + lg * 8) * 2;
+  }
+  // B: pieces lane-linear per wave, 16-B chunks XOR-swizzled as in the LDS-DMA kernels
+  const i32x4 rs_b = buffer_rsrc(a.w + (long)n0 * a.K, (uint32_t)min((long)(a.N - n0) * a.K * 2, cap));
+  int bvo[BI];
+#pragma unroll
+  for (int p = 0; p < BI; ++p) {
+    const int q = (wid * BI + p) * 64 + lane, row = q / 8;
+    const int lc = swz_bk<64>(row, q % 8) - row * 8;  // logical chunk stored at physical chunk q % 8
+    bvo[p] = (row * a.K + lc * 8) * 2;
+  }
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+  auto issue_b = [&](int kt) {
+    uint4* base = lds + (kt % 3) * STAGE;
+#pragma unroll
+    for (int p = 0; p < BI; ++p)
+      ls_raw_buffer_load_lds(rs_b, (__attribute__((address_space(3))) void*)(base + (wid_u * BI + p) * 64), 16, bvo[p],
+                             kt * 128, 0, 0);
+  };
+  bf16x8 ar[2][2][FM];  // [register set][k-step][fragment]
+  auto load_a = [&](int kt, bf16x8 (&r)[2][FM]) {
+    const bool two = a.C2 && kt * 64 >= a.C1;
+    const int soff = (two ? kt * 64 - a.C1 : kt * 64) * 2;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        r[ks][i] = __builtin_bit_cast(bf16x8, ls_raw_buffer_load_v4(two ? rs_a2 : rs_a1, two ? avo2[i] : avo1[i],
+                                                                    soff + ks * 64, 0));
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  issue_b(0);
+  if (kt1 > 1) issue_b(1);
+  load_a(0, ar[0]);
+  // K-tile kt from register set CUR; B of kt lands in stage kt % 3 (issued two K-tiles ahead)
+  auto body = [&](int kt, auto cur_tag) {
+    constexpr int CUR = decltype(cur_tag)::value;
+    if (kt + 2 < kt1) issue_b(kt + 2);
+    if (kt + 1 < kt1) load_a(kt + 1, ar[CUR ^ 1]);
+    // B(kt) and A(kt) landed: the VMEM instructions younger than A(kt) are B(kt + 2) and A(kt + 1)
+    if (kt + 2 < kt1) wait_vm<BI + 2 * FM>();
+    else if (kt + 1 < kt1) wait_vm<2 * FM>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const uint4* cur = lds + (kt % 3) * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 bfr[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bfr[j] = __builtin_bit_cast(bf16x8, cur[swz_bk<64>(wn * WTN + j * 16 + l16, ks * 4 + lg)]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[CUR][ks][i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // stage kt % 3 free for B(kt + 3)
+    asm volatile("" ::: "memory");
+  };
+  int kt = 0;
+  for (; kt + 1 < kt1; kt += 2) {
+    body(kt, std::integral_constant<int, 0>{});
+    body(kt + 1, std::integral_constant<int, 1>{});
+  }
+  if (kt < kt1) body(kt, std::integral_constant<int, 0>{});
+  store_tile<BM, BN, WM, WN, EPI>(a, acc, (float*)lds, m0, n0, 0);
+}
+
 // 256-row tile, 8 waves (2 M x 4 N), each wave 128 x BN/4 (FM = 8 fragments of
 // 16 rows x FN of 16 cols): 1.5x the MFMAs per LDS fragment read of the 4-wave
 // 64 x 64 wave tile.  One block per CU (128 KB of LDS: two 64-KB stages at
@@ -2447,6 +2563,14 @@ static void launch_rs(const ConvArgs& a, int grid, hipStream_t s) {
   LS_SET_MAX_DYN_SHM((conv_gemm_rs_kernel<BM, BN, WM, WN, KS, EPI>), (int)shm);
   conv_gemm_rs_kernel<BM, BN, WM, WN, KS, EPI><<<grid, WM * WN * 64, shm, s>>>(a);
 }
+static bool g_areg = getenv("LS_GEMM_AREG") ? atoi(getenv("LS_GEMM_AREG")) != 0 : false;  // A/B switch: 1x1 A in registers
+
+template <int BM, int BN, int WM, int WN, int EPI>
+static void launch_areg(const ConvArgs& a, int grid, hipStream_t s) {
+  const size_t shm = std::max<size_t>((size_t)3 * BN * 8 * 16, (size_t)(BM / WM) * (BN + 4) * 4);
+  LS_SET_MAX_DYN_SHM((conv_gemm_areg_kernel<BM, BN, WM, WN, EPI>), (int)shm);
+  conv_gemm_areg_kernel<BM, BN, WM, WN, EPI><<<grid, WM * WN * 64, shm, s>>>(a);
+}
 static bool g_no_buf_ups = getenv("LS_GEMM_UPS_GLDS") != nullptr;  // A/B switch: ... for upsampling convs only
 
 // operand DMA through buffer descriptors: 1x1 with K == Cin, Cin % 64 == 0; tap-major 3x3,
@@ -2467,6 +2591,15 @@ static void launch_dma(const ConvArgs& a, int grid, hipStream_t s) {
     if (g_bk == 32) { launch_dma1<BM, BN, WM, WN, KS, TAPU, 4, 32, EPI_ANY>(a, grid, s); return; }
   }
   if constexpr (KS == 1 || TAPU) {
+    if constexpr (KS == 1) {
+      if (g_areg && buf_dma_ok(a, 1) && a.split == 1) {
+        switch (epi_kind(a)) {
+          case EPI_PLAIN: launch_areg<BM, BN, WM, WN, EPI_PLAIN>(a, grid, s); return;
+          case EPI_GEGLU: launch_areg<BM, BN, WM, WN, EPI_GEGLU>(a, grid, s); return;
+          default: launch_areg<BM, BN, WM, WN, EPI_ANY>(a, grid, s); return;
+        }
+      }
+    }
     if (g_rs && buf_dma_ok(a, KS) && a.split == 1) {
       switch (epi_kind(a)) {
         case EPI_PLAIN: launch_rs<BM, BN, WM, WN, KS, EPI_PLAIN>(a, grid, s); return;
@@ -2705,6 +2838,7 @@ extern "C" int ls_set_tuning(int32_t key, int32_t value) {
     case 8: g_halo = value != 0; return LS_OK;
     case 12: g_halo_rp = value != 0; return LS_OK;
     case 13: g_halo_bn128 = value != 0; return LS_OK;
+    case 14: g_areg = value != 0; return LS_OK;
     case 9: attn_set_attn6(value != 0); return LS_OK;
     case 10: g_t256 = value; return LS_OK;
     case 11: g_rs = value; return LS_OK;

@@ -101,5 +101,6 @@ if __name__ == "__main__":
         lib.ls_set_tuning(11, 1 if "rs" in parts else 0)
         lib.ls_set_tuning(12, 0 if "nohrp" in parts else 1)
         lib.ls_set_tuning(13, 1 if "bn128" in parts else 0)
+        lib.ls_set_tuning(14, 1 if "areg" in parts else 0)
         TORCH_REF = "torch" in parts
         run(arg, scale=int(sc or 1))
