@@ -2479,10 +2479,25 @@ static void launch_rowblock2(const ConvArgs& a, int grid, hipStream_t s) {
   gemm_rowblock_kernel<KT, FM, FN, FLAGS><<<grid, 512, shm, s>>>(a);
 }
 
+// A/B switch (tuning key 15): K = 640 with two 16-row fragments per wave (256-row blocks, half
+// the W-fragment LDS reads per MFMA, 160 A registers)
+static bool g_rb640_fm2 = getenv("LS_RB640_FM2") != nullptr;
+
+static bool rb640_fm2(int flags);
+
 template <int FLAGS>
 static void launch_rowblock1(const ConvArgs& a, int grid, hipStream_t s) {
-  if (a.K == 320) launch_rowblock2<10, 2, FLAGS>(a, grid, s);
-  else launch_rowblock2<20, 1, FLAGS>(a, grid, s);
+  if (a.K == 320) {
+    launch_rowblock2<10, 2, FLAGS>(a, grid, s);
+    return;
+  }
+  if constexpr (!(FLAGS & (RB_STATS | RB_GNCS))) {  // (the statistics epilogues spill at FM 2)
+    if (rb640_fm2(FLAGS)) {
+      launch_rowblock2<20, 2, FLAGS>(a, grid, s);
+      return;
+    }
+  }
+  launch_rowblock2<20, 1, FLAGS>(a, grid, s);
 }
 
 // returns false when no instance matches (the caller then uses the tiled kernels)
@@ -2492,15 +2507,18 @@ static const int kRowblockInstances[] = {0, RB_LN, RB_LN | RB_RV, RB_RES, RB_LN 
 
 // the row-block instance flags for this call, or -1; the row-block grid goes to
 // *ntm / *ntn only (the caller's tiled grid in a.ntm / a.ntn stays valid for a fallback)
+static bool rb640_fm2(int flags) { return g_rb640_fm2 && !(flags & (RB_STATS | RB_GNCS)); }
+
 static int rowblock_flags(const ConvArgs& a, int* ntm_out, int* ntn_out) {
-  const int bm = a.K == 320 ? 256 : 128;
+  const int flags = (a.ln_mr ? RB_LN : 0) | (a.res ? RB_RES : 0) | (a.rowvec ? RB_RV : 0) |
+                    (a.act == LS_ACT_GEGLU ? RB_GEGLU : 0) | (a.stats_out ? RB_STATS : 0) | (a.cs_out ? RB_GNCS : 0) |
+                    (a.aff_scale ? RB_AFF : 0);
+  const int bm = a.K == 320 || rb640_fm2(flags) ? 256 : 128;
+  if (a.M % bm) return -1;
   const int ntm = a.M / bm, nch = a.N / 32;
   const int ntn = std::max(1, std::min(nch, (256 + ntm - 1) / ntm));
   if (a.stats_out && ntn != 1) return -1;  // fused statistics need whole rows per block
   if (a.cs_out && (bm % CS_ROWS || ntn != 1)) return -1;
-  const int flags = (a.ln_mr ? RB_LN : 0) | (a.res ? RB_RES : 0) | (a.rowvec ? RB_RV : 0) |
-                    (a.act == LS_ACT_GEGLU ? RB_GEGLU : 0) | (a.stats_out ? RB_STATS : 0) | (a.cs_out ? RB_GNCS : 0) |
-                    (a.aff_scale ? RB_AFF : 0);
   for (int f : kRowblockInstances)
     if (f == flags) {
       *ntm_out = ntm;
@@ -2839,6 +2857,7 @@ extern "C" int ls_set_tuning(int32_t key, int32_t value) {
     case 12: g_halo_rp = value != 0; return LS_OK;
     case 13: g_halo_bn128 = value != 0; return LS_OK;
     case 14: g_areg = value != 0; return LS_OK;
+    case 15: g_rb640_fm2 = value != 0; return LS_OK;
     case 9: attn_set_attn6(value != 0); return LS_OK;
     case 10: g_t256 = value; return LS_OK;
     case 11: g_rs = value; return LS_OK;
