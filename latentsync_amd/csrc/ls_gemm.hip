@@ -2479,9 +2479,10 @@ static void launch_rowblock2(const ConvArgs& a, int grid, hipStream_t s) {
   gemm_rowblock_kernel<KT, FM, FN, FLAGS><<<grid, 512, shm, s>>>(a);
 }
 
-// A/B switch (tuning key 15): K = 640 with two 16-row fragments per wave (256-row blocks, half
-// the W-fragment LDS reads per MFMA, 160 A registers)
-static bool g_rb640_fm2 = getenv("LS_RB640_FM2") != nullptr;
+// K = 640 with two 16-row fragments per wave (256-row blocks, half the W-fragment LDS reads
+// per MFMA, 160 A registers): default since r04x (step 215.3 -> 212.2 ms at 48 windows, three
+// same-box alternations); tuning key 15 / LS_RB640_FM2=0: one fragment per wave
+static bool g_rb640_fm2 = getenv("LS_RB640_FM2") == nullptr || atoi(getenv("LS_RB640_FM2")) != 0;
 
 static bool rb640_fm2(int flags);
 
