@@ -457,24 +457,6 @@ __global__ void __launch_bounds__(256, (KC >= 5 && !ONE) ? 1 : 2) attn3_kernel(A
 template <int N>
 __device__ __forceinline__ void attn_wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
-// s_waitcnt vmcnt(n) for a wave-uniform runtime n (an immediate per case)
-__device__ __forceinline__ void attn_wait_vm_dyn(int n) {
-  switch (n) {
-    case 0: attn_wait_vm<0>(); break;
-    case 1: attn_wait_vm<1>(); break;
-    case 2: attn_wait_vm<2>(); break;
-    case 3: attn_wait_vm<3>(); break;
-    case 4: attn_wait_vm<4>(); break;
-    case 5: attn_wait_vm<5>(); break;
-    case 6: attn_wait_vm<6>(); break;
-    case 7: attn_wait_vm<7>(); break;
-    case 8: attn_wait_vm<8>(); break;
-    case 9: attn_wait_vm<9>(); break;
-    case 10: attn_wait_vm<10>(); break;
-    default: attn_wait_vm<0>(); break;
-  }
-}
-
 // XCD-aware order (blocks b and b + 8 share an XCD under round-robin dispatch): every
 // XCD gets a contiguous range of logical blocks, so the query blocks of one (batch,
 // head) -- which read the same K/V tiles -- run together on one L2.
@@ -725,6 +707,7 @@ static int launch_attn5(const AttnArgs& a, int batch, int heads, hipStream_t s) 
   return check_launch("attn5_kernel");
 }
 
+#ifdef LS_DIAG_KERNELS  // measured and rejected: diagnostics build only
 // attn6: the d = 40 self attention (UNet 32x32 level; 64x64 at configs[4]) on
 // v_mfma_f32_32x32x16_bf16.  attn5 is issue-bound, not MFMA-bound: per 64-key tile and
 // wave it issues 64 v_exp_f32 (8 cycles each) beside 56 16x16x32 MFMAs that each hold the
@@ -981,6 +964,8 @@ static int launch_attn6(const AttnArgs& a, int batch, int heads, hipStream_t s) 
   attn6_kernel<DSUM><<<(int)nblk, 256, shm, s>>>(a, nqb, heads);
   return check_launch("attn6_kernel");
 }
+
+#endif  // LS_DIAG_KERNELS
 
 // attnw: wide heads -- the SD-VAE mid-block attention (1 head, d = 512, N = h w tokens;
 // diffusers Attention).  Replaces attn_kernel<512,4> (0.068 of the
@@ -1895,9 +1880,13 @@ static bool g_attn_v1 = getenv("LS_ATTN_V1") != nullptr;  // A/B switch: force t
 static bool g_attn_v3 = getenv("LS_ATTN_V3") != nullptr;  // A/B switch: attn3 for d = 40 too
 // A/B switch: d = 40 self attention on attn6 (32x32x16); measured 3 % slower than attn5 at 48
 // windows (1670 vs 1620 us per call, profiles/r04b_attn_ab.txt), so attn5 stays the default
+#ifdef LS_DIAG_KERNELS
 static bool g_attn6 = getenv("LS_ATTN6") != nullptr;
+#else
+static bool g_attn6 = false;
+#endif
 namespace ls {
-void attn_set_attn6(bool on) { g_attn6 = on; }  // ls_set_tuning key 9
+void attn_set_attn6(bool on) { g_attn6 = on; }  // ls_set_tuning key 9 (diagnostics build)
 }
 static bool g_attnw_off = getenv("LS_ATTNW_OFF") != nullptr;  // A/B switch: d = 512 on attn_kernel
 static bool g_seq_valu = getenv("LS_ATTN_SEQ_VALU") != nullptr;  // A/B switch: dot-product short-sequence kernel
@@ -1999,7 +1988,10 @@ extern "C" int ls_attention(const ls_attn_desc* d, void* stream) {
     // queries per wave, row sums from the PV MFMA; short key sets (the 50 audio tokens)
     // and other head dims: attn3 (register-staged tiles)
     if (D == 40 && !g_attn_v3 && d->nk > 128 && ((long)(d->nk - 1) * std::max(d->k_si, d->v_si) + D) * 2 < (1L << 31))
-      return g_attn6 ? launch_attn6<40>(a, d->batch, d->heads, s) : launch_attn5<2, 3, 40, 4>(a, d->batch, d->heads, s);
+#ifdef LS_DIAG_KERNELS
+      if (g_attn6) return launch_attn6<40>(a, d->batch, d->heads, s);
+#endif
+      return launch_attn5<2, 3, 40, 4>(a, d->batch, d->heads, s);
     if (D == 40) return launch_attn3<2, 3, 40>(a, d->batch, d->heads, s);
     switch ((D + 15) / 16) {
       case 1: case 2: return launch_attn3<1, 2, 0>(a, d->batch, d->heads, s);

@@ -1020,6 +1020,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_gemm_dma_kernel(ConvArgs a)
   store_tile<BM, BN, WM, WN, EPI>(a, acc, (float*)lds, m0, n0, z);
 }
 
+#ifdef LS_DIAG_KERNELS  // measured and rejected: diagnostics build only
 // Register-staged variant of conv_gemm_dma_kernel's BUF path (A/B switch LS_GEMM_RS=1):
 // the same buffer-descriptor offsets, but each 16-B operand piece goes through a VGPR
 // (buffer_load_dwordx4, then ds_write_b128 into the slot the LDS-DMA would have written)
@@ -1238,6 +1239,8 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_gemm_areg_kernel(ConvArgs a
   store_tile<BM, BN, WM, WN, EPI>(a, acc, (float*)lds, m0, n0, 0);
 }
 
+#endif  // LS_DIAG_KERNELS
+
 // 256-row tile, 8 waves (2 M x 4 N), each wave 128 x BN/4 (FM = 8 fragments of
 // 16 rows x FN of 16 cols): 1.5x the MFMAs per LDS fragment read of the 4-wave
 // 64 x 64 wave tile.  One block per CU (128 KB of LDS: two 64-KB stages at
@@ -1385,6 +1388,7 @@ __global__ void __launch_bounds__(512) conv_gemm_big_kernel(ConvArgs a) {
   store_tile<BM, BN, WM, WN, EPI>(a, acc, (float*)lds, m0, n0, z);
 }
 
+#ifdef LS_DIAG_KERNELS  // measured and rejected: diagnostics build only
 // 256 x 256 x 64 tile, 8 waves (2 M x 4 N, 128 x 64 per wave), phased schedule
 // (after the guide's 8-phase template): each K-tile runs as 4 phases, one per
 // 64 x 32 quadrant of the wave tile (16 MFMAs).  A phase issues the fragment
@@ -1670,6 +1674,8 @@ __global__ void __launch_bounds__(512) conv_gemm_big4_kernel(ConvArgs a) {
   asm volatile("" ::: "memory");
   store_tile<BM, BN, WM, WN>(a, acc, (float*)lds, m0, n0, z);
 }
+
+#endif  // LS_DIAG_KERNELS
 
 // split-K reduction + epilogue: one thread per 8 output columns
 __global__ void splitk_reduce_kernel(ConvArgs a) {
@@ -2492,7 +2498,7 @@ static void launch_rowblock1(const ConvArgs& a, int grid, hipStream_t s) {
     launch_rowblock2<10, 2, FLAGS>(a, grid, s);
     return;
   }
-  if constexpr (!(FLAGS & (RB_STATS | RB_GNCS))) {  // (the statistics epilogues spill at FM 2)
+  if constexpr (!(FLAGS & (RB_STATS | RB_GNCS | RB_AFF))) {  // (the statistics epilogues spill at FM 2)
     if (rb640_fm2(FLAGS)) {
       launch_rowblock2<20, 2, FLAGS>(a, grid, s);
       return;
@@ -2508,7 +2514,9 @@ static const int kRowblockInstances[] = {0, RB_LN, RB_LN | RB_RV, RB_RES, RB_LN 
 
 // the row-block instance flags for this call, or -1; the row-block grid goes to
 // *ntm / *ntn only (the caller's tiled grid in a.ntm / a.ntn stays valid for a fallback)
-static bool rb640_fm2(int flags) { return g_rb640_fm2 && !(flags & (RB_STATS | RB_GNCS)); }
+// (not with the GroupNorm affine: a block looks its sample up once, and rowblock_ok only
+// guarantees pix_per_sample % 128 == 0 at K = 640)
+static bool rb640_fm2(int flags) { return g_rb640_fm2 && !(flags & (RB_STATS | RB_GNCS | RB_AFF)); }
 
 static int rowblock_flags(const ConvArgs& a, int* ntm_out, int* ntn_out) {
   const int flags = (a.ln_mr ? RB_LN : 0) | (a.res ? RB_RES : 0) | (a.rowvec ? RB_RV : 0) |
@@ -2574,6 +2582,7 @@ static void launch_dma1(const ConvArgs& a, int grid, hipStream_t s) {
 }
 
 static bool g_no_buf_dma = getenv("LS_GEMM_GLDS") != nullptr;  // A/B switch: global_load_lds addressing
+#ifdef LS_DIAG_KERNELS  // measured and rejected: diagnostics build only
 static int g_rs = getenv("LS_GEMM_RS") ? atoi(getenv("LS_GEMM_RS")) : 0;  // A/B switch: register-staged buffer loads
 
 template <int BM, int BN, int WM, int WN, int KS, int EPI>
@@ -2590,6 +2599,8 @@ static void launch_areg(const ConvArgs& a, int grid, hipStream_t s) {
   LS_SET_MAX_DYN_SHM((conv_gemm_areg_kernel<BM, BN, WM, WN, EPI>), (int)shm);
   conv_gemm_areg_kernel<BM, BN, WM, WN, EPI><<<grid, WM * WN * 64, shm, s>>>(a);
 }
+#endif  // LS_DIAG_KERNELS
+
 static bool g_no_buf_ups = getenv("LS_GEMM_UPS_GLDS") != nullptr;  // A/B switch: ... for upsampling convs only
 
 // operand DMA through buffer descriptors: 1x1 with K == Cin, Cin % 64 == 0; tap-major 3x3,
@@ -2606,10 +2617,13 @@ template <int BM, int BN, int WM, int WN, int KS, bool TAPU>
 static void launch_dma(const ConvArgs& a, int grid, hipStream_t s) {
   // (BK 32 tuning mode: only tiles whose 16-B operand pieces divide over the threads --
   // 128 x 160 has 640 B pieces for 256 threads and would leave B rows unloaded)
+#ifdef LS_DIAG_KERNELS
   if constexpr (BN >= 64 && (BN * 4) % (WM * WN * 64) == 0 && (BM * 4) % (WM * WN * 64) == 0) {
     if (g_bk == 32) { launch_dma1<BM, BN, WM, WN, KS, TAPU, 4, 32, EPI_ANY>(a, grid, s); return; }
   }
+#endif
   if constexpr (KS == 1 || TAPU) {
+#ifdef LS_DIAG_KERNELS
     if constexpr (KS == 1) {
       if (g_areg && buf_dma_ok(a, 1) && a.split == 1) {
         switch (epi_kind(a)) {
@@ -2626,6 +2640,7 @@ static void launch_dma(const ConvArgs& a, int grid, hipStream_t s) {
         default: launch_rs<BM, BN, WM, WN, KS, EPI_ANY>(a, grid, s); return;
       }
     }
+#endif
     if (buf_dma_ok(a, KS)) {
       switch (epi_kind(a)) {
         case EPI_PLAIN: launch_dma1<BM, BN, WM, WN, KS, TAPU, 2, 64, EPI_PLAIN, true>(a, grid, s); return;
@@ -2666,6 +2681,7 @@ static void launch_big1(const ConvArgs& a, int grid, hipStream_t s) {
   }
 }
 
+#ifdef LS_DIAG_KERNELS  // measured and rejected: diagnostics build only
 template <int KS, bool TAPU>
 static void launch_big4(const ConvArgs& a, int grid, hipStream_t s) {
   const size_t shm = std::max<size_t>((size_t)4 * (256 + 256) * 4 * 16, (size_t)128 * (256 + 4) * 4);
@@ -2679,6 +2695,8 @@ static void launch_p8_1(const ConvArgs& a, int grid, hipStream_t s) {
   LS_SET_MAX_DYN_SHM((conv_gemm_p8_kernel<KS, TAPU>), (int)shm);
   conv_gemm_p8_kernel<KS, TAPU><<<grid, 512, shm, s>>>(a);
 }
+
+#endif  // LS_DIAG_KERNELS
 
 template <int BN>
 static void launch_big(const ConvArgs& a, int ks, bool tapu, int grid, hipStream_t s) {
@@ -2767,10 +2785,13 @@ static void launch_halo(const ConvArgs& a, int tw, hipStream_t s) {
   launch_halo1<16>(a, s);
 }
 
+#ifdef LS_DIAG_KERNELS  // measured and rejected: diagnostics build only
 // 256 x 128 tiles (8 waves as 4 x 2, 64 x 64 each) with a 3-stage LDS ring (147 KB) for the
 // short-K linears (K <= 1280, N % 128 == 0): two K-tiles of operand DMA in flight instead of
 // one.  (A/B switch LS_GEMM_T256=0/1; tile id 260.  256 x 160 would leave 2.5 B pieces per thread.)
 static int g_t256 = getenv("LS_GEMM_T256") ? atoi(getenv("LS_GEMM_T256")) : 0;
+
+#endif  // LS_DIAG_KERNELS
 
 static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split) {
   if (!d || !d->x1 || !d->w || !d->y) return fail(LS_ERR_INVALID, "ls_conv2d: null pointer");
@@ -2820,9 +2841,11 @@ static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split
                                   {257, 256}, {258, 256}, {128, 160}, {259, 160}};
     t.bm = tb[g_force_tile][0]; t.bn = tb[g_force_tile][1]; t.split = g_force_split ? g_force_split : 1;
   }
+#ifdef LS_DIAG_KERNELS
   if (g_t256 && !g_force_tile && d->ksize == 1 && a.ktiles <= 20 && d->N % 128 == 0 && !d->aff_scale &&
       M % 256 == 0 && d->K == Cin && Cin % 64 == 0 && d->C1 % 64 == 0)
     t = {260, 128, 1};
+#endif
   a.ntm = cdiv(M, t.bm > 256 ? 256 : t.bm); a.ntn = cdiv(d->N, t.bn);  // 257..260 = 256-row kernel variants
   // grouped raster (LS_GEMM_GM=g, g row-bands per group): it cuts the wide linears' L2-miss
   // fetch (GEGLU W1 at 8x8 3.6 -> 1.3 GB per call) but measured +0.4 ms per 32-window step
@@ -2848,20 +2871,35 @@ namespace ls { void attn_set_attn6(bool on); }
 extern "C" int ls_set_tuning(int32_t key, int32_t value) {
   switch (key) {
     case 1: g_force_regstage = value != 0; return LS_OK;
-    case 2: if (value < 0 || value > 9) return fail(LS_ERR_INVALID, "tile id 0..9"); g_force_tile = value; return LS_OK;
+    case 2:
+#ifndef LS_DIAG_KERNELS
+      if (value == 7 || value == 8) return fail(LS_ERR_INVALID, "tile ids 7 / 8: diagnostics build only");
+#endif
+      if (value < 0 || value > 9) return fail(LS_ERR_INVALID, "tile id 0..9");
+      g_force_tile = value;
+      return LS_OK;
     case 3: g_force_split = value; return LS_OK;
     case 4: g_ablate = value; return LS_OK;
+#ifdef LS_DIAG_KERNELS
     case 5: if (value != 32 && value != 64) return fail(LS_ERR_INVALID, "BK 32 or 64"); g_bk = value; return LS_OK;
+#endif
     case 6: g_rowblock = value != 0; return LS_OK;
     case 7: g_rowblock640 = value != 0; return LS_OK;
     case 8: g_halo = value != 0; return LS_OK;
     case 12: g_halo_rp = value != 0; return LS_OK;
     case 13: g_halo_bn128 = value != 0; return LS_OK;
-    case 14: g_areg = value != 0; return LS_OK;
     case 15: g_rb640_fm2 = value != 0; return LS_OK;
-    case 9: attn_set_attn6(value != 0); return LS_OK;
+    case 9:
+#ifndef LS_DIAG_KERNELS
+      if (value) return fail(LS_ERR_INVALID, "attn6: diagnostics build only");
+#endif
+      attn_set_attn6(value != 0);
+      return LS_OK;
+#ifdef LS_DIAG_KERNELS
     case 10: g_t256 = value; return LS_OK;
     case 11: g_rs = value; return LS_OK;
+    case 14: g_areg = value != 0; return LS_OK;
+#endif
     default: return fail(LS_ERR_INVALID, "ls_set_tuning: unknown key");
   }
 }
@@ -2941,6 +2979,7 @@ extern "C" int ls_conv2d(const ls_conv_desc* d, void* stream) {
   const bool cs_epi = cs && a.split == 1 && vec && !(t.bm == 128 && t.bn == 32) && t.bm != 64 &&
                       (t.bm < 256 || (t.bm == 260 && epi_kind(a) == EPI_PLAIN));
   if (cs_epi) a.cs_out = cs;
+#ifdef LS_DIAG_KERNELS
   if (t.bm == 260) {  // 256 x 128, 3-stage ring (short-K linears)
     switch (epi_kind(a)) {
       case EPI_PLAIN: launch_dma1<256, 128, 4, 2, 1, false, 3, 64, EPI_PLAIN, true>(a, grid, s); break;
@@ -2953,7 +2992,9 @@ extern "C" int ls_conv2d(const ls_conv_desc* d, void* stream) {
   } else if (t.bm == 258 && !a.aff_scale && !g_force_regstage && (d->ksize == 1 || tapu)) {  // 4-stage BK 32
     if (d->ksize == 1) launch_big4<1, false>(a, grid, s);
     else launch_big4<3, true>(a, grid, s);
-  } else if (t.bm == 256 && !a.aff_scale && !g_force_regstage) {
+  } else
+#endif
+  if (t.bm == 256 && !a.aff_scale && !g_force_regstage) {
     if (t.bn == 256) launch_big<256>(a, d->ksize, tapu, grid, s);
     else launch_big<128>(a, d->ksize, tapu, grid, s);
   } else if (t.bm == 128 && t.bn == 128) launch_cfg<128, 128, 2, 2>(a, d->ksize, tapu, grid, s);

@@ -21,6 +21,7 @@ parity harness requires (SURVEY.md §7 "RNG").
 """
 import collections
 import math
+import time
 import os
 
 import numpy as np
@@ -155,6 +156,7 @@ class WindowEngine:
         self.out_u8 = z(F_, R, R, 3, dt=torch.uint8)
         self.use_graphs = use_graphs
         self.graphs = None
+        self.capture_s = None
 
     # -- the three phases --------------------------------------------------------
     def _encode(self):
@@ -182,7 +184,9 @@ class WindowEngine:
     def capture(self):
         """Warm up eagerly once, then capture the three phases as hipGraphs.  Graphs
         of engines closed or collected earlier are destroyed first, outside the
-        capture; an engine collected DURING the capture only retires its graphs."""
+        capture; an engine collected DURING the capture only retires its graphs.
+        The wall time of warm-up + capture is kept in ``capture_s``."""
+        t0 = time.perf_counter()
         self._encode()
         self._step()
         self._decode()
@@ -202,6 +206,7 @@ class WindowEngine:
             raise
         torch.cuda.synchronize(self.device)
         self.graphs = graphs
+        self.capture_s = time.perf_counter() - t0
 
     def _retire(self):
         g = self.__dict__.get("graphs")
@@ -273,6 +278,26 @@ class WindowEngine:
 # --------------------------------------------------------------------------
 
 
+# Engine sizes (windows per UNet call) a clip's full windows are rounded up to, so clips of
+# different lengths share captured engines (a new size costs a warm-up run + three graph
+# captures, WindowEngine.capture_s); padding windows run and are discarded.
+WINDOW_BUCKETS = (1, 2, 4, 8, 16, 24, 32, 40, 48)
+
+
+def plan_window_batches(full, windows_per_batch):
+    """Split the full windows `full` (indices) into batches for one engine size E:
+    E = the smallest bucket (WINDOW_BUCKETS below `windows_per_batch`, plus
+    `windows_per_batch` itself) that holds ceil(len / ceil(len / windows_per_batch))
+    windows; batches of E consecutive windows, the last one short (the caller pads it).
+    Returns (E, batches); (0, []) for no full window."""
+    if not full:
+        return 0, []
+    cap = max(1, int(windows_per_batch))
+    per = math.ceil(len(full) / math.ceil(len(full) / cap))
+    E = min(b for b in sorted({b for b in WINDOW_BUCKETS if b < cap} | {cap}) if b >= per)
+    return E, [list(full[b:b + E]) for b in range(0, len(full), E)]
+
+
 class LipsyncPipeline:
     """Drop-in for LipsyncPipeline(vae, audio_encoder, denoising_unet, scheduler)."""
 
@@ -286,9 +311,10 @@ class LipsyncPipeline:
         self._engines = collections.OrderedDict()
         # Independent windows batched per UNet call (identical per-window math; see
         # tests/test_gpu_pipeline.py::test_windows_batched_equal_separate).  A clip's
-        # full windows on this rank are split into ceil(n / windows_per_batch) equal
-        # batches, so every request runs at the benchmarked operating point (48, bench.py)
-        # or as close to it as the clip allows; engines are kept in a small LRU cache.
+        # full windows on this rank run through ONE engine whose size is the batch size
+        # rounded up to a bucket (plan_window_batches: at most 48, the benchmarked
+        # operating point of bench.py), short batches padded, so clips of different
+        # lengths share captured engines; engines are kept in a small LRU cache.
         self.windows_per_batch = 48
         self.max_engines = 3
 
@@ -376,19 +402,18 @@ class LipsyncPipeline:
         # last window runs alone (eagerly: it happens once per clip).  A per-step
         # callback sees one window's latents at a time, as in the reference.
         full = [i for i in mine if size[i] == num_frames]
-        nb = 1 if callback is not None else max(1, int(self.windows_per_batch))
-        nb = math.ceil(len(full) / math.ceil(len(full) / nb)) if full else 1  # equal batches
-        batches = [full[b:b + nb] for b in range(0, len(full), nb)] + [[i] for i in mine if size[i] < num_frames]
+        E, batches = plan_window_batches(full, 1 if callback is not None else self.windows_per_batch)
+        batches = [(E, b) for b in batches] + [(1, [i]) for i in mine if size[i] < num_frames]
         res = {}
-        for wins in batches:
+        for E, wins in batches:
             Fw = size[wins[0]]
-            eng = self.engine(Fw, R, num_inference_steps, guidance_scale, use_graphs=Fw == num_frames,
-                              windows=len(wins))
-            sls = [slice(i * num_frames, i * num_frames + Fw) for i in wins]
+            eng = self.engine(Fw, R, num_inference_steps, guidance_scale, use_graphs=Fw == num_frames, windows=E)
+            run = wins + [wins[-1]] * (E - len(wins))  # padding windows: computed, discarded
+            sls = [slice(i * num_frames, i * num_frames + Fw) for i in run]
             cat = lambda xs: torch.cat([x.to(self.device) for x in xs])
             eng.load(cat([faces_u8[sl] for sl in sls]), mask, cat([whisper_chunks[sl] for sl in sls]),
                      cat([all_latents[:, :, sl] for sl in sls]),
-                     cat([noise[i][0] for i in wins]), cat([noise[i][1] for i in wins]))
+                     cat([noise[i][0] for i in run]), cat([noise[i][1] for i in run]))
             eng.run(callback=callback, callback_steps=callback_steps)
             for k, i in enumerate(wins):
                 fs = slice(k * Fw, (k + 1) * Fw)

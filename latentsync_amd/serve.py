@@ -156,7 +156,8 @@ def _worker_main(rank, factory, job_kw, conn):
 
 class WorkerDied(RuntimeError):
     """The GPU worker process ended (fault, abort, OOM kill) or missed the request
-    timeout while serving a request; it has been replaced by a fresh process."""
+    timeout while serving a request; a fresh process has been launched in its place
+    (or the replacement itself failed to start: the message says which)."""
 
 
 class ProcessWorker:
@@ -167,13 +168,17 @@ class ProcessWorker:
     fault kills the whole server): a request that does not finish within
     `request_timeout` seconds, or whose worker dies under it, fails with WorkerDied
     and the worker is replaced by a freshly SPAWNED child (never a re-exec of a
-    process that touched the GPU), so the next request routed here is served."""
+    process that touched the GPU), so the next request routed here is served.  The
+    failed request is answered at once; the replacement loads in the background and
+    the next request waits for its 'ready' (a replacement that fails to start fails
+    that request with WorkerDied too, and is retried on the one after)."""
 
     def __init__(self, rank, factory, request_timeout=1800.0, start_timeout=900.0, **job_kw):
         self.rank, self.factory, self.job_kw = rank, factory, job_kw
         self.request_timeout, self.start_timeout = request_timeout, start_timeout
         self.proc = self.conn = None
         self.restarts = 0
+        self._unready = False  # a replacement child was launched and has not reported 'ready'
 
     def launch(self):
         """Spawn the child; `wait_ready` collects its 'ready' (so N GPUs load together)."""
@@ -208,11 +213,21 @@ class ProcessWorker:
             self.conn.close()
 
     def _replace(self):
+        """Kill the child and launch its replacement without waiting for it to load."""
         self._kill()
         self.restarts += 1
-        self.start()
+        self.launch()
+        self._unready = True
 
     def _call(self, payload):
+        if self._unready:  # the replacement launched after the previous failure
+            try:
+                self.wait_ready()
+                self._unready = False
+            except RuntimeError as e:
+                self._replace()
+                return "dead", (f"GPU worker {self.rank}: the replacement child did not start ({e}); "
+                                f"request {payload.get('id')!r} not served, another replacement launched")
         try:
             self.conn.send(payload)
             if not self.conn.poll(self.request_timeout):
@@ -223,7 +238,7 @@ class ProcessWorker:
             self.proc.join(timeout=5)
             why = f"died (exit code {self.proc.exitcode})"
         self._replace()
-        return "dead", f"GPU worker {self.rank} {why} while serving request {payload.get('id')!r}; replaced"
+        return "dead", f"GPU worker {self.rank} {why} while serving request {payload.get('id')!r}; replacement launched"
 
     async def run(self, payload):
         loop = asyncio.get_running_loop()

@@ -20,6 +20,9 @@ SHAPES = [  # (name, n_img, H, Cin, Cout, ksize, act)
     ("vae conv 256>512 64^2", 16, 64, 256, 512, 3, 0), ("vae conv 256 128^2", 16, 128, 256, 256, 3, 0),
     ("vae conv 128>256 128^2", 16, 128, 128, 256, 3, 0),
     ("out1 640->640", 16, 16, 640, 640, 1, 0), ("out2 1280->1280", 16, 8, 1280, 1280, 1, 0),
+    ("sc2a 640->1280", 16, 8, 640, 1280, 1, 0), ("sc2b 1920->1280", 16, 8, 1920, 1280, 1, 0),
+    ("sc2c 2560->1280", 16, 8, 2560, 1280, 1, 0), ("out3 1280->1280 4x4", 16, 4, 1280, 1280, 1, 0),
+    ("ff2_3 5120->1280 4x4", 16, 4, 5120, 1280, 1, 0), ("sc3 2560->1280 4x4", 16, 4, 2560, 1280, 1, 0),
 ]
 
 

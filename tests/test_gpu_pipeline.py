@@ -190,3 +190,41 @@ def test_engines_dropped_during_capture(gpu):
         out2 = eng.run().cpu()  # a closed engine captures again
         assert torch.equal(out, out2)
         eng.close()
+
+
+def test_clip_lengths_share_one_engine(gpu, monkeypatch):
+    """Clips of 10 and 11 windows run through ONE captured engine (16 windows: the bucket,
+    pipeline.plan_window_batches; padding windows computed and discarded).  The windows the
+    two clips have in common come out bit-identical (same engine, same per-window inputs:
+    the padding windows never mix into a real one), and window 0 matches the oracle."""
+    from latentsync_amd.pipeline import LipsyncPipeline
+    Fr, Rr, steps = 4, 64, 2
+    h = Rr // 8
+    unet = UNet3DConditionModel(**TINY_MODEL).init_weights(19).to("cuda").eval()
+    vae = AutoencoderKL(block_out_channels=(32, 64, 64, 64)).init_weights(20).to("cuda")
+    monkeypatch.setitem(R.VAE_CFG, "block_out_channels", (32, 64, 64, 64))
+    pipe = LipsyncPipeline(vae, None, unet, DDIMScheduler(**SCHED))
+    g = torch.Generator().manual_seed(21)
+    n_max = 11
+    N = n_max * Fr
+    faces = (torch.rand((N, 3, Rr, Rr), generator=g) * 255).to(torch.uint8)
+    mask = load_fixed_mask(Rr)
+    audio = torch.randn((N, 50, 384), generator=g)
+    init = torch.randn((1, 4, 1, h, h), generator=g).repeat(1, 1, N, 1, 1)
+    noise = [(torch.randn((Fr, 4, h, h), generator=g), torch.randn((Fr, 4, h, h), generator=g)) for _ in range(n_max)]
+    outs = {}
+    for n_win in (10, 11):
+        n = n_win * Fr
+        outs[n_win], _ = pipe.run_windows(faces[:n], audio[:n].cuda(), mask, Fr, steps, 1.0,
+                                          all_latents=init[:, :, :n].cuda(),
+                                          vae_noise=lambda i: (noise[i][0].cuda(), noise[i][1].cuda()))
+        assert outs[n_win].shape == (n, 3, Rr, Rr)
+    assert list(k[-1] for k in pipe._engines) == [16], list(pipe._engines)
+    eng = next(iter(pipe._engines.values()))
+    print(f"engine of 16 windows: warm-up + capture {eng.capture_s:.3f} s")
+    assert torch.equal(outs[10], outs[11][:10 * Fr])
+    ref = R.pipeline_window(unet.state_dict(), dict(unet.config), vae._sd, faces[:Fr], mask, audio[:Fr],
+                            init[:, :, :1], noise[0][0], noise[0][1], num_steps=steps, guidance_scale=1.0)
+    e = rel_err(outs[11][:Fr].cpu(), ref)
+    print("bucketed engine window 0 vs oracle", e)
+    assert e < 3e-2

@@ -118,5 +118,6 @@ def test_process_request_through_gpu_worker(tmp_path, monkeypatch):
         d = np.abs(got - ref_u8)
         print("served window", w, "rel", e, "max", d.max(), "p99.9", np.percentile(d, 99.9))
         # the window tolerance of tests/test_gpu_pipeline.py (tiny random-weight UNet, CFG 1.5,
-        # 2 steps: rel-L2 < 3e-2) plus a coarse per-pixel bound
-        assert e < 3e-2 and d.max() <= 12
+        # 2 steps: rel-L2 < 3e-2) plus per-pixel bounds on the like-for-like (truncated) uint8
+        # frames: max <= 12 levels, 99.9th percentile <= 5
+        assert e < 3e-2 and d.max() <= 12 and np.percentile(d, 99.9) <= 5
