@@ -48,7 +48,7 @@ def _deps():
 # tests/test_build_guards.py checks that every kernel with a non-zero counted wait in csrc/ is listed.
 COUNTED_VMCNT = ("gemm_rowblock_kernel", "conv_gemm_dma_kernel", "attn5_kernel", "attn8_kernel", "tattn_fused_kernel",
                  "attnw_kernel", "conv3x3_halo_kernel", "attn6_kernel", "conv_gemm_p8_kernel", "conv_gemm_big4_kernel",
-                 "conv_gemm_areg_kernel")
+                 "conv_gemm_areg_kernel", "ff_pair_kernel")
 
 
 def _spills(stderr):
@@ -101,6 +101,8 @@ def _compile(src, obj, dep_time):
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         return obj, r.stderr
+    with open(obj[:-2] + ".remarks", "w") as f:  # per-kernel VGPR / AGPR / occupancy (scripts/kernel_regs.py)
+        f.write(r.stderr)
     bad = _spills(r.stderr)
     if bad:
         os.remove(obj)

@@ -182,6 +182,191 @@ __global__ void __launch_bounds__(512, 1) ff_fused_kernel(FFArgs a) {
   }
 }
 
+// ff_pair_kernel (round 5): the same FeedForward with each W fragment read from LDS feeding
+// TWO MFMAs.  ff_fused_kernel's waves own 16 rows, so every 1-KB W1 / W2 fragment it reads
+// serves one 16x16x32 MFMA: 480 KB of LDS reads per chunk and CU against 1920 MFMA cycles
+// per SIMD, and with the fragment-read -> MFMA dependency neither the matrix pipe (38 %
+// busy) nor the LDS (40 %) is kept full (PMC, profiles/r05d_ff_pmc.txt).  Here a PAIR of
+// waves owns 32 rows (two 16-row fragments, A in registers for both: 80 VGPRs) and splits
+// the work by columns:
+//   * GEMM1: wave h of the pair computes the h / g tiles of inner columns 16 h .. 16 h + 15
+//     of the chunk (W1 tiles 2h, 2h + 1) for both row fragments: 20 fragment reads, 40 MFMAs;
+//   * GEGLU -> 4 bf16 per lane and row fragment: inner columns 16 h + 4 lg .. + 3;
+//   * the pair exchanges them through LDS (8 B per lane and row fragment), so each wave
+//     holds GEMM2's full 32-wide B operand -- k-slots 4 lg .. + 3 from wave 0 and 16 + 4 lg
+//     .. + 3 from wave 1, the order pack_ff_w2 already puts the W2 columns in;
+//   * GEMM2: wave h accumulates output columns 160 h .. 160 h + 159 (10 tiles) for both row
+//     fragments: 10 fragment reads, 20 MFMAs.
+// 0.5 KB of LDS reads per MFMA instead of 1, the same MFMAs, GELUs and W DMA per row.  The
+// exchange's barrier is also where W1 of chunk c + 2 is issued into the stage just read (as
+// the W1 images of the stage just read).
+template <int C, int I, int PD1 = 2, int PD2 = 6>
+__global__ void __launch_bounds__(512, 1) ff_pair_kernel(FFArgs a) {
+  constexpr int KT = C / 32;              // GEMM1 k-steps
+  constexpr int NCH = I / 32;             // inner chunks
+  constexpr int WIMG = 64 * (C / 64) * 8; // uint4: W1 chunk, C/64 images of [64 rows][8 pieces]
+  constexpr int W2IMG = C * 4;            // uint4: W2 chunk, [C rows][4 pieces]
+  constexpr int STAGE = WIMG + W2IMG;
+  constexpr int NT2 = C / 32;             // output tiles per wave (half of C / 16)
+  constexpr int PW1 = WIMG / 512;         // W1 pieces per thread per chunk
+  constexpr int UW2 = W2IMG / 64;         // W2 wave-instructions per chunk
+  static_assert(WIMG % 512 == 0 && W2IMG % 64 == 0 && C % 64 == 0 && I % 32 == 0, "ff_pair shape");
+  static_assert(PD1 >= 1 && PD1 <= KT && PD2 >= PD1 && PD2 <= NT2, "prefetch depths");
+  extern __shared__ __attribute__((aligned(16))) uint4 lds[];  // [2][STAGE], b1 (2I fp32), exchange
+  float* b1s = (float*)(lds + 2 * STAGE);
+  uint2* xch = (uint2*)(b1s + 2 * I);    // [4 pairs][2 halves][2 row fragments][64 lanes]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l16 = lane & 15, lg = lane >> 4;
+  const int pr = wid >> 1, h = wid & 1;  // pair, half
+  const long row0 = (long)blockIdx.x * 128 + pr * 32 + l16;  // row of fragment 0 (fragment 1: + 16)
+
+  for (int i = tid; i < 2 * I / 4; i += 512) ((float4*)b1s)[i] = ((const float4*)a.b1)[i];
+
+  auto issue_w1 = [&](int c, int st) {
+    uint4* dst = lds + st * STAGE;
+#pragma unroll
+    for (int p = 0; p < PW1; ++p) {
+      const int q = p * 512 + tid, r = (q >> 3) & 63, pc = q & 7;
+      const int lc = pc ^ ((r >> 1) & 7);
+      glds16(a.w1 + (long)(c * 64 + r) * C + p * 64 + lc * 8, dst + p * 512 + wid * 64);
+    }
+  };
+  auto issue_w2 = [&](int c, int st) {
+    uint4* dst = lds + st * STAGE;
+    for (int u = wid; u < UW2; u += 8) glds16(a.w2 + ((long)c * W2IMG + u * 64 + lane) * 8, dst + WIMG + u * 64);
+  };
+  issue_w1(0, 0);
+  issue_w2(0, 0);
+
+  // A rows of both fragments -> registers, LayerNorm in place
+  bf16x8 ar[2][KT];
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const long row = row0 + 16 * f;
+    const bool live = row < a.M;
+    const u16* src = a.x + (live ? row : 0) * a.ldx + lg * 8;
+#pragma unroll
+    for (int s = 0; s < KT; ++s)
+      ar[f][s] = live ? *(const bf16x8*)(src + s * 32) : __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0));
+    const float2 mr = live ? *(const float2*)(a.ln_mr + 2 * row) : make_float2(0.f, 0.f);
+    const float rstd = mr.y, nmr = -mr.x * mr.y;
+#pragma unroll
+    for (int s = 0; s < KT; ++s) {
+      bf16x8 v = ar[f][s];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (__bf16)fmaf((float)v[e], rstd, nmr);
+      ar[f][s] = v;
+    }
+  }
+  if (NCH > 1) issue_w1(1, 1);  // W1 runs a half chunk ahead of W2: refilled at the exchange barrier
+
+  f32x4 out[NT2][2];
+#pragma unroll
+  for (int t = 0; t < NT2; ++t) out[t][0] = out[t][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int p2 = lg ^ (((l16 >> 3) & 1) << 1);  // this lane's physical W2 piece
+  uint2* const xmine = xch + ((pr * 2 + h) * 2) * 64 + lane;
+  const uint2* const xpart = xch + ((pr * 2 + (h ^ 1)) * 2) * 64 + lane;
+
+  for (int c = 0; c < NCH; ++c) {
+    if (c + 1 < NCH) wait_vm<PW1>();  // W1 + W2 of chunk c landed; W1 of c + 1 may fly
+    else wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // everyone's; the other stage's W2 (chunk c - 1) is no longer read
+    asm volatile("" ::: "memory");
+    if (c + 1 < NCH) issue_w2(c + 1, (c + 1) & 1);
+    const uint4* cur = lds + (c & 1) * STAGE;
+
+    // GEMM1: tiles 2h (h) and 2h + 1 (g) of the chunk, both row fragments
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) acc[t][0] = acc[t][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    auto frag = [&](int s, int t) {
+      return __builtin_bit_cast(bf16x8, cur[(s >> 1) * 512 + swz_bk<64>((2 * h + t) * 16 + l16, (s & 1) * 4 + lg)]);
+    };
+    const uint4* w2 = cur + WIMG + (size_t)(h * NT2 * 16) * 4;  // this wave's 160 output rows of W2
+    bf16x8 wf[PD1][2];
+#pragma unroll
+    for (int q = 0; q < PD1; ++q)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) wf[q][t] = frag(q, t);
+    uint4 w2q[PD2];
+#pragma unroll
+    for (int s = 0; s < KT; ++s) {
+      const int sl = s % PD1;
+      const bf16x8 c0 = wf[sl][0], c1 = wf[sl][1];
+      if (s + PD1 < KT) {
+        wf[sl][0] = frag(s + PD1, 0);
+        wf[sl][1] = frag(s + PD1, 1);
+      } else if (s + PD1 - KT < PD2) {
+        w2q[s + PD1 - KT] = w2[((s + PD1 - KT) * 16 + l16) * 4 + p2];
+      }
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        acc[0][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c0, ar[f][s], acc[0][f], 0, 0, 0);
+        acc[1][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c1, ar[f][s], acc[1][f], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int q = PD1; q < PD2; ++q) w2q[q] = w2[(q * 16 + l16) * 4 + p2];
+    // GEGLU of inner columns 16 h + 4 lg .. + 3 -> this wave's half of the B operand
+    const float* bb = b1s + c * 64 + 32 * h + 4 * lg;
+    const float4 bh = *(const float4*)(bb), bg = *(const float4*)(bb + 16);
+    const float hb[4] = {bh.x, bh.y, bh.z, bh.w}, gb[4] = {bg.x, bg.y, bg.z, bg.w};
+    uint2 mine[2];
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      float g4[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) g4[r] = (acc[0][f][r] + hb[r]) * gelu_erf(acc[1][f][r] + gb[r]);
+      mine[f] = make_uint2(pack2(g4[0], g4[1]), pack2(g4[2], g4[3]));
+      xmine[f * 64] = mine[f];
+    }
+    // the pair's exchange; every wave's GEMM1 reads of this stage's W1 images have retired too,
+    // so they are refilled with chunk c + 2
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (c + 2 < NCH) issue_w1(c + 2, c & 1);
+    bf16x8 gv[2];
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      const uint2 other = xpart[f * 64];
+      const uint4 q = h == 0 ? make_uint4(mine[f].x, mine[f].y, other.x, other.y)
+                             : make_uint4(other.x, other.y, mine[f].x, mine[f].y);
+      gv[f] = __builtin_bit_cast(bf16x8, q);
+    }
+    // GEMM2: out^T[160 h + 16 t + 4 lg + r][row] += W2[160 h + 16 t + l16][chunk k-slots] . G^T
+#pragma unroll
+    for (int t = 0; t < NT2; ++t) {
+      const bf16x8 wv = __builtin_bit_cast(bf16x8, w2q[t % PD2]);
+      if (t + PD2 < NT2) w2q[t % PD2] = w2[((t + PD2) * 16 + l16) * 4 + p2];
+      out[t][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, gv[0], out[t][0], 0, 0, 0);
+      out[t][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, gv[1], out[t][1], 0, 0, 0);
+    }
+  }
+
+  // y = out + b2 + x for this wave's 160 columns of both row fragments
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const long row = row0 + 16 * f;
+    if (row >= a.M) continue;
+    const u16* xr = a.x + row * a.ldx;
+    u16* yr = a.y + row * a.ldy;
+#pragma unroll
+    for (int t = 0; t < NT2; ++t) {
+      const int col = C / 2 * h + 16 * t + 4 * lg;
+      const float4 b = *(const float4*)(a.b2 + col);
+      const uint2 rs = *(const uint2*)(xr + col);
+      const float o0 = out[t][f][0] + b.x + __uint_as_float(rs.x << 16);
+      const float o1 = out[t][f][1] + b.y + __uint_as_float(rs.x & 0xffff0000u);
+      const float o2 = out[t][f][2] + b.z + __uint_as_float(rs.y << 16);
+      const float o3 = out[t][f][3] + b.w + __uint_as_float(rs.y & 0xffff0000u);
+      *(uint2*)(yr + col) = make_uint2(pack2(o0, o1), pack2(o2, o3));
+    }
+  }
+}
+
 }  // namespace ls
 
 using namespace ls;
@@ -200,6 +385,13 @@ extern "C" int ls_feedforward(const ls_ff_desc* d, void* stream) {
   a.x = (const u16*)d->x; a.ln_mr = d->ln_rowstats; a.w1 = (const u16*)d->w1; a.b1 = d->b1;
   a.w2 = (const u16*)d->w2; a.b2 = d->b2; a.y = (u16*)d->y; a.M = d->M; a.ldx = d->ldx; a.ldy = d->ldy;
   constexpr int C = 320, I = 1280;
+  static const bool v1 = getenv("LS_FF_V1") != nullptr && atoi(getenv("LS_FF_V1")) != 0;  // A/B switch
+  if (!v1) {
+    const size_t shm = (size_t)2 * (64 * (C / 64) * 8 + C * 4) * 16 + 2 * I * sizeof(float) + 4 * 2 * 2 * 64 * 8;
+    LS_SET_MAX_DYN_SHM((ff_pair_kernel<C, I>), (int)shm);
+    ff_pair_kernel<C, I><<<(unsigned)((d->M + 127) / 128), 512, shm, (hipStream_t)stream>>>(a);
+    return check_launch("ff_pair_kernel");
+  }
   const size_t shm = (size_t)2 * (64 * (C / 64) * 8 + C * 4) * 16 + 2 * I * sizeof(float);
   LS_SET_MAX_DYN_SHM((ff_fused_kernel<C, I>), (int)shm);
   ff_fused_kernel<C, I><<<(unsigned)((d->M + 127) / 128), 512, shm, (hipStream_t)stream>>>(a);

@@ -247,13 +247,56 @@ __host__ __device__ constexpr bool cs_tile_fits() {
   return BM != 256 && BM % CS_ROWS == 0 && CS_ROWS % (BM / WM) == 0 && WM * WN * 64 >= BN;
 }
 
+// Thread geometry of the single-pass epilogue: a thread owns one 8-column chunk of the
+// tile (CPRW chunk columns per row), RPI rows per iteration, ITER iterations per wave-row pass.
+template <int BM, int BN, int WM, int WN>
+struct EpiGeo {
+  static constexpr int NT = WM * WN * 64, WTM = BM / WM, CPRW = BN / 8, RPI = NT / CPRW;
+  static constexpr int ITER = (WTM + RPI - 1) / RPI;
+};
+// the residual chunks of one wave-row pass (the per-row side input worth prefetching; the
+// LayerNorm row statistics of a folded GEMM are loaded in the pass)
+template <int ITER>
+struct EpiSide {
+  uint4 rs[ITER];
+};
+
+// tile-local row -> output row (RW: see store_tile_plain)
+template <int RW>
+__device__ __forceinline__ int epi_out_row(const ConvArgs& a, int m0, long m0r, int lr) {
+  if constexpr (RW > 0) return (int)(m0r + (long)(lr / RW) * a.Wo + lr % RW);
+  else return m0 + lr;
+}
+
+// issue the residual loads of wave-row pass p (global loads into registers; the consumer's
+// s_waitcnt is the compiler's): one HBM round trip per pass, issued a pass (or, from the
+// DMA kernel's last K-tile, the whole final K-tile) before it is consumed
+template <int BM, int BN, int WM, int WN, int RW = 0>
+__device__ __forceinline__ void epi_side_load(const ConvArgs& a, int m0, int n0, long m0r, int tid, int p,
+                                              EpiSide<EpiGeo<BM, BN, WM, WN>::ITER>& sd) {
+  using G = EpiGeo<BM, BN, WM, WN>;
+  const int c8 = (tid % G::CPRW) * 8, r0 = tid / G::CPRW;
+  const int col = n0 + c8;
+  const bool cok = (r0 < G::RPI) && col < a.N;
+#pragma unroll
+  for (int it = 0; it < G::ITER; ++it) {
+    const int rl = r0 + it * G::RPI, row = epi_out_row<RW>(a, m0, m0r, p * G::WTM + rl);
+    const bool ok = cok && rl < G::WTM && row < a.M;
+    sd.rs[it] = make_uint4(0, 0, 0, 0);
+    if (ok && a.res) sd.rs[it] = *(const uint4*)(a.res + (long)row * a.ldr + col);
+  }
+}
+
 // CSF: the column sums also for a 256-row tile whose wave rows are 64 (the halo conv);
 // RW > 0: the tile's rows are BM / RW segments of RW consecutive output pixels, one per
 // image row (the halo conv's TH x TW tiles); m0 is then the tile's VIRTUAL first row
-// (GroupNorm slots) and m0r the real first row.
-template <int BM, int BN, int WM, int WN, bool GEN, bool CSF = false, int RW = 0>
-__device__ __forceinline__ void store_tile_plain(const ConvArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
-                                                 float* st, int m0, int n0, long m0r = 0, int tid_in = -1) {
+// (GroupNorm slots) and m0r the real first row.  PRE: pass 0's side inputs were loaded by
+// the caller (epi_side_load during its last K-tile) into `pre`.  Pass p + 1's side inputs
+// are issued right after pass p's staging barrier, so only the first pass waits on HBM.
+template <int BM, int BN, int WM, int WN, bool GEN, bool CSF = false, int RW = 0, bool PRE = false, bool PIPE = true>
+__device__ __forceinline__ void store_tile_plain_pre(const ConvArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
+                                                     float* st, int m0, int n0, long m0r, int tid_in,
+                                                     const EpiSide<EpiGeo<BM, BN, WM, WN>::ITER>& pre) {
   constexpr int NT = WM * WN * 64, WTM = BM / WM, SP = BN + 4;
   constexpr int CPRW = BN / 8;                 // chunk columns per tile row
   constexpr int RPI = NT / CPRW;               // rows per iteration
@@ -261,10 +304,7 @@ __device__ __forceinline__ void store_tile_plain(const ConvArgs& a, f32x4 (&acc)
   constexpr bool CSOK = CSF || cs_tile_fits<BM, BN, WM, WN>();
   static_assert(!CSF || (CS_ROWS % WTM == 0 && NT >= BN), "column-sum slots of whole wave rows");
   // tile-local row -> output row
-  auto out_row = [&](int lr) -> int {
-    if constexpr (RW > 0) return (int)(m0r + (long)(lr / RW) * a.Wo + lr % RW);
-    else return m0 + lr;
-  };
+  auto out_row = [&](int lr) -> int { return epi_out_row<RW>(a, m0, m0r, lr); };
   const int tid = tid_in >= 0 ? tid_in : (int)threadIdx.x;  // (a caller in a loop passes an opaque copy)
   const int c8 = (tid % CPRW) * 8, r0 = tid / CPRW;
   const int col = n0 + c8;
@@ -289,21 +329,25 @@ __device__ __forceinline__ void store_tile_plain(const ConvArgs& a, f32x4 (&acc)
   if (cok && a.ln_mr) load8f(a.ln_cs + col, cs);
   // no LayerNorm fold, no per-row row vector, unit output scale: the short path
   const bool plain = !a.ln_mr && !(a.rowvec && !rv_tile) && a.out_scale == 1.f && !(a.ablate & 8);
+  EpiSide<ITER> cur;
+  if constexpr (PRE) cur = pre;
+  else if constexpr (PIPE) epi_side_load<BM, BN, WM, WN, RW>(a, m0, n0, m0r, tid, 0, cur);
 #pragma unroll 1
   for (int p = 0; p < WM; ++p) {
     stage_acc<BM, BN, WM, WN>(acc, st, p, tid);
+    // (no pipelining: this pass's residual after its staging writes, as the accumulators
+    // it staged are dead -- the 256 x 256 tile has no registers to spare before that)
+    if constexpr (!PIPE && !PRE) epi_side_load<BM, BN, WM, WN, RW>(a, m0, n0, m0r, tid, p, cur);
     float2 mr[ITER];
-    uint4 rs[ITER];
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
       const int rl = r0 + it * RPI, row = out_row(p * WTM + rl);
-      const bool ok = cok && rl < WTM && row < a.M;
       mr[it] = make_float2(0.f, 1.f);
-      rs[it] = make_uint4(0, 0, 0, 0);
-      if (ok && a.ln_mr) mr[it] = *(const float2*)(a.ln_mr + 2L * row);
-      if (ok && a.res) rs[it] = *(const uint4*)(a.res + (long)row * a.ldr + col);
+      if (cok && rl < WTM && row < a.M && a.ln_mr) mr[it] = *(const float2*)(a.ln_mr + 2L * row);
     }
     __syncthreads();
+    EpiSide<ITER> nxt;
+    if (PIPE && p + 1 < WM) epi_side_load<BM, BN, WM, WN, RW>(a, m0, n0, m0r, tid, p + 1, nxt);
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
       const int rl = r0 + it * RPI, row = out_row(p * WTM + rl);
@@ -312,7 +356,7 @@ __device__ __forceinline__ void store_tile_plain(const ConvArgs& a, f32x4 (&acc)
       const float4 s0 = *(const float4*)s, s1 = *(const float4*)(s + 4);
       float v[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
       float r8[8];
-      unpack8(rs[it], r8);
+      unpack8(cur.rs[it], r8);
       if (plain) {  // (block-uniform) bias (+ the tile's row vector) + residual: 2 VALU per value
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (v[j] + bb[j]) + r8[j];
@@ -374,7 +418,20 @@ __device__ __forceinline__ void store_tile_plain(const ConvArgs& a, f32x4 (&acc)
       }
       __syncthreads();
     }
+    if constexpr (PIPE) {
+      if (p + 1 < WM) cur = nxt;
+    }
   }
+}
+
+template <int BM, int BN, int WM, int WN, bool GEN, bool CSF = false, int RW = 0>
+__device__ __forceinline__ void store_tile_plain(const ConvArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
+                                                 float* st, int m0, int n0, long m0r = 0, int tid_in = -1) {
+  // (the 8-wave 256 x 256 tile runs at the 256-VGPR limit: its next pass's residual loads
+  // would spill, so they stay in the pass)
+  EpiSide<EpiGeo<BM, BN, WM, WN>::ITER> none;
+  store_tile_plain_pre<BM, BN, WM, WN, GEN, CSF, RW, false, !(BM == 256 && WM == 2)>(a, acc, st, m0, n0, m0r, tid_in,
+                                                                                     none);
 }
 
 // GEGLU variant: a thread owns one 8-wide OUTPUT chunk, i.e. packed columns
@@ -947,6 +1004,9 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_gemm_dma_kernel(ConvArgs a)
   constexpr bool ILV = false;  // (A/B: BUF && NST == 2)
   constexpr bool ILV_SGB = false;  // explicit interleave (sched_group_barrier): see DESIGN
   int stage = 0;
+  // the plain epilogue's first-pass side inputs (residual / LayerNorm rows), loaded during
+  // the last K-tile so their HBM latency hides under its MFMAs
+  EpiSide<EpiGeo<BM, BN, WM, WN>::ITER> pre;
   // one K-tile; IS: issue the next K-tile's DMA inside it (ILV).  (Peeling the last K-tile so
   // that the DMA and the MFMAs share one basic block made the register allocator rotate the
   // accumulators through AGPR moves, ~90 per K-tile: not kept.)
@@ -960,6 +1020,9 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_gemm_dma_kernel(ConvArgs a)
     else wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if constexpr (EPI == EPI_PLAIN) {
+      if (kt == kt1 - 1) epi_side_load<BM, BN, WM, WN>(a, m0, n0, 0, tid, 0, pre);
+    }
     const uint4* cur = lds + stage * STAGE;
     bf16x8 af[KSTEPS][FM], bfr[KSTEPS][FN];
 #pragma unroll
@@ -1017,6 +1080,13 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_gemm_dma_kernel(ConvArgs a)
     return;
   }
 #endif
+  if constexpr (EPI == EPI_PLAIN) {
+    if (kt0 < kt1) {
+      store_tile_plain_pre<BM, BN, WM, WN, false, BM == 256 && WM == 4, 0, true>(a, acc, (float*)lds, m0, n0, 0, -1,
+                                                                                 pre);
+      return;
+    }
+  }
   store_tile<BM, BN, WM, WN, EPI>(a, acc, (float*)lds, m0, n0, z);
 }
 
@@ -2130,7 +2200,9 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
 //     the 9 taps need (brute-forced over the lane groups; the GEMMs' ((row >> 1) & 7)
 //     swizzle is 2-way there).  Halo rows are TW + 8 pixels long (== 0 mod 8), so the
 //     swizzle phase of every fragment of a wave equals its first fragment's: one address
-//     computation per (tap, k-step) and lane, fragment offsets are immediates;
+//     computation per (tap, k-step) and lane, fragment offsets are immediates (round 5
+//     measured the compact TW + 2 row with a column-based swizzle: it frees 28 KB of LDS,
+//     but the third weight slot at BN 160 that room was for spills 30 VGPRs, so not kept);
 //   * the 9 taps of the chunk then run from that image: tap (kh, kw) shifts the read by
 //     kh (TW + 8) + kw pixels; the weight K-tile of each tap ([BN][64], channel-chunk-major
 //     packing) streams through an NSW-slot LDS ring by LDS-DMA, NSW - 1 taps ahead;
@@ -2146,7 +2218,7 @@ struct HaloCfg {
   static constexpr int P = TW + 8;                       // halo row pitch (pixels), 0 mod 8
   static constexpr int HALO = (TH + 2) * P * 8;          // uint4 per halo image
   static constexpr int WSLOT = BN * 8;                   // uint4 per weight ring slot (BN x 64 k)
-  static constexpr int NSW = BN <= 128 ? 3 : 2;          // weight ring slots
+  static constexpr int NSW = BN <= 128 ? 3 : 2;          // weight ring slots (3 at BN 160: 30 VGPRs of spills)
   static constexpr int NHL = (HALO + 511) / 512;         // halo loads per thread per chunk
   static constexpr int DPT = (WSLOT + 511) / 512;        // weight DMAs per thread per tap
   static constexpr int FN = BN / 32;                     // 16-column fragments per wave
@@ -2167,15 +2239,13 @@ __host__ __device__ constexpr int halo_issue(int t, int nhl, bool gn) {
   return t == 0 ? hb_lo(1, nhl) + (gn ? 1 : 0) : t == 3 ? hb_lo(2, nhl) - hb_lo(1, nhl) : t == 6 ? nhl - hb_lo(2, nhl) : 0;
 }
 
-// RP: the halo pieces are enumerated over the (TH + 2) x (TW + 2) pixels the taps read
-// (2592 pieces for 16 x 16: 5.06 per thread) instead of over the padded image
-// (HALO = 3456: 6.75), so a wave transforms ~25 % fewer pieces; each piece's LDS slot is
-// then per piece (hdst[]), not one base + j * 512
-template <int TW, int BN, bool GN, bool CSF, bool RP = false>
+// Halo pieces: the (TH + 2) x (TW + 2) pixels the taps read x 8 16-B chunks (2592 pieces at
+// 16 x 16: 5.06 per thread); piece j of a thread has its own LDS slot hdst[j].
+template <int TW, int BN, bool GN, bool CSF>
 __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
   using HC = HaloCfg<TW, BN>;
   constexpr int TH = HC::TH, P = HC::P, HALO = HC::HALO, WSLOT = HC::WSLOT, NSW = HC::NSW;
-  constexpr int NPC = RP ? (TH + 2) * (TW + 2) * 8 : HALO;  // pieces per chunk
+  constexpr int NPC = (TH + 2) * (TW + 2) * 8;  // pieces per chunk (the read pixels)
   constexpr int NHL = (NPC + 511) / 512, DPT = HC::DPT, FM = 4, FN = HC::FN, WTN = BN / 2;
   constexpr int HB = (NHL + 2) / 3;  // largest batch
   extern __shared__ __attribute__((aligned(16))) uint4 lds_dyn[];
@@ -2200,27 +2270,20 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
   const int nchunk = a.Cin / 64;
   const int G = 9 * nchunk;  // taps in all
 
-  // ---- this thread's halo pieces: q = j*512 + tid -> pixel q / 8 = 64 j + tid / 8, logical
-  // 16-B chunk tid & 7; the swizzled slot is j*512 + hdst0 (64 j == 0 mod 8 keeps the phase)
+  // ---- this thread's halo pieces: q = j*512 + tid -> read pixel q / 8 (row-major over the
+  // (TH + 2) x (TW + 2) pixels the taps read), logical 16-B chunk tid & 7; its slot in the
+  // padded image: row hr, column hcol + 3, the chunk swizzled by (slot & 7)
   const int hc8 = tid & 7;
-  const int hdst0 = (tid >> 3) * 8 + (hc8 ^ ((tid >> 3) & 7));
   int hpix[NHL];  // pixel index within the image, or -1 (outside: zeros)
-  int hdst[RP ? NHL : 1];
+  int hdst[NHL];
 #pragma unroll
   for (int j = 0; j < NHL; ++j) {
     const int q = j * 512 + tid, hp = q >> 3;
-    if constexpr (RP) {
-      const int hr = hp / (TW + 2), hcol = hp - hr * (TW + 2);
-      const int y = y0 - 1 + hr, x = x0 - 1 + hcol;
-      const int slot = hr * P + hcol + 3;
-      hdst[j] = slot * 8 + (hc8 ^ (slot & 7));
-      hpix[j] = q < NPC && y >= 0 && y < a.H && x >= 0 && x < a.W ? y * a.W + x : -1;
-    } else {
-      const int hr = hp / P, hcol = hp - hr * P;
-      const int y = y0 - 1 + hr, x = x0 - 4 + hcol;
-      const bool ok = q < HALO && hcol >= 3 && hcol <= TW + 4 && y >= 0 && y < a.H && x >= 0 && x < a.W;
-      hpix[j] = ok ? y * a.W + x : -1;
-    }
+    const int hr = hp / (TW + 2), hcol = hp - hr * (TW + 2);
+    const int y = y0 - 1 + hr, x = x0 - 1 + hcol;
+    const int slot = hr * P + hcol + 3;
+    hdst[j] = slot * 8 + (hc8 ^ (slot & 7));
+    hpix[j] = q < NPC && y >= 0 && y < a.H && x >= 0 && x < a.W ? y * a.W + x : -1;
   }
   const uint32_t cap = 0x7FFFFFFFu;
   const i32x4 rs1 = buffer_rsrc(a.x1 + img * HW * a.ld1, (uint32_t)min((long)HW * a.ld1 * 2, (long)cap));
@@ -2254,7 +2317,6 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
   };
   auto store_halo = [&](int buf, int b) {
     uint4* const hb0 = hbuf + buf * HALO;
-    uint4* dst = hb0 + hdst0;
     const int j0 = hb_lo(b, NHL), j1 = hb_lo(b + 1, NHL);
     float4 gsc[2], gsh[2];
     if constexpr (GN) {  // this thread's 8 channels (chunk parity buf)
@@ -2276,8 +2338,7 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
           v = pack8(f);
         }
       }
-      if constexpr (RP) hb0[hdst[j]] = v;
-      else dst[j * 512] = v;
+      hb0[hdst[j]] = v;
     }
   };
 
@@ -2292,17 +2353,22 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
     const int lc = pc ^ ((row >> 1) & 7);
     wvo[j] = ((q < WSLOT ? row : 0) * a.K + lc * 8) * 2;
   }
-  auto issue_w = [&](int g) {
-    uint4* slot = wbuf + (g % NSW) * WSLOT;
+  // ring slot of tap g: with 3 slots, (9 ci + t) % 3 == t % 3 is known per tap at compile time
+  auto wslot = [&](int g, int t) { return NSW == 3 ? t % 3 : g % NSW; };
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+  auto issue_w = [&](int g, int sl) {
+    uint4* slot = wbuf + sl * WSLOT;
 #pragma unroll
     for (int j = 0; j < DPT; ++j) {
-      const bool live = j * 512 + wid * 64 < WSLOT;  // wave-uniform
-      ls_raw_buffer_load_lds(rs_w, (__attribute__((address_space(3))) void*)(live ? slot + j * 512 + wid * 64 : dummy), 16,
-                             wvo[j], g * 128, 0, 0);
+      const bool live = j * 512 + wid_u * 64 < WSLOT;  // wave-uniform
+      ls_raw_buffer_load_lds(rs_w, (__attribute__((address_space(3))) void*)(live ? slot + j * 512 + wid_u * 64 : dummy),
+                             16, wvo[j], g * 128, 0, 0);
     }
   };
 
-  // ---- A fragment addressing: output pixel p = 64 wm + 16 i + l16 of the patch
+  // ---- A fragment addressing: output pixel p = 64 wm + 16 i + l16 of the patch (TW 16:
+  // fragment i is patch row 4 wm + i, column l16)
+  static_assert(TW == 16, "fragment i = one patch row");
   const int p0 = 64 * wm + l16;
   const int hp0 = (p0 / TW) * P + (p0 % TW) + 3;  // halo pixel of fragment 0 at tap (0, 0)
 
@@ -2313,7 +2379,7 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   // prologue: weights of taps 0 .. NSW - 2, halo of chunk 0
-  for (int g = 0; g < NSW - 1 && g < G; ++g) issue_w(g);
+  for (int g = 0; g < NSW - 1 && g < G; ++g) issue_w(g, g % NSW);
   if constexpr (GN) {
     load_par(0);
     store_par(0);
@@ -2328,7 +2394,7 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
   bf16x8 apf[2][FM];  // A fragments of the current tap (both k-steps)
   auto read_a = [&](const uint4* hb, int tt) {  // (tt compile-time after inlining)
     const int hpt = hp0 + (tt / 3) * P + tt % 3;
-    const int sw = hpt & 7;
+    const int sw = hpt & 7;  // (P == 0 mod 8: the phase of every fragment of the wave)
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int base = hpt * 8 + ((ks * 4 + lg) ^ sw);
@@ -2350,14 +2416,14 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (g + NSW - 1 < G) issue_w(g + NSW - 1);
+    if (g + NSW - 1 < G) issue_w(g + NSW - 1, wslot(g + NSW - 1, t + NSW - 1));
     if constexpr (!LAST) {
       if constexpr (GN && t == 1) store_par(ci + 1);  // read at taps 3 / 6 / 8, past a barrier
       if constexpr (t == 3 || t == 6) store_halo((ci + 1) & 1, t / 3 - 1);
       if constexpr (t == 0 || t == 3 || t == 6) load_halo(ci + 1, t / 3);
     }
     const uint4* hb = hbuf + (ci & 1) * HALO;
-    const uint4* wb = wbuf + (g % NSW) * WSLOT;
+    const uint4* wb = wbuf + wslot(g, t) * WSLOT;
     // A fragments of tap t: at t = 0 read here; for t > 0 read at the end of tap t - 1 (the
     // halo image is stable within a chunk), so after this tap's barrier only the weight
     // fragments stand between the wave and its MFMAs, and the LDS array serves 10 reads per
@@ -2410,6 +2476,8 @@ static int g_force_tile = 0, g_force_split = 0, g_bk = 64;
 static int g_ablate = getenv("LS_GEMM_ABLATE") ? atoi(getenv("LS_GEMM_ABLATE")) : 0;
 
 struct TileCfg { int bm, bn, split; };
+// A/B switch (LS_GEMM_BIG1280=0): the N = 1280 linears back on 128 x 160 tiles
+static bool g_big1280 = getenv("LS_GEMM_BIG1280") == nullptr || atoi(getenv("LS_GEMM_BIG1280")) != 0;
 
 // Tile + split-K choice by a small cost model.  A CU runs up to R blocks of a tile
 // at once (LDS-limited: 2 for the 4-wave 128-row tiles, 1 for the 8-wave 256x256);
@@ -2429,9 +2497,13 @@ static TileCfg pick_tile(long M, int N, int ktiles, bool allow_split, bool big_o
     if (N <= 32 && c.bn != 32) continue;
     if (c.bm == 256) {
       if (!big_ok || N < 256) continue;
-      // linears: 256x256 only on wide N (GEGLU W1, fused q|k|v at 1280 channels) or when
-      // 160 does not divide N (the VAE's 512); 3x3 convs: the cost model decides
-      if (ksize == 1 && ((N % 256 != 0 && N < 1920) || (N <= 1280 && N % 160 == 0))) continue;
+      // linears: 256x256 only on wide N (GEGLU W1, fused q|k|v, and N = 1280: the 8x8 / 4x4
+      // levels' projections, FF2 and shortcuts, 7-16 % faster than 128x160 on every one of
+      // them, profiles/r05c_n1280.txt) or when 160 does not divide N (the VAE's 512); 3x3
+      // convs: the cost model decides
+      if (ksize == 1 && ((N % 256 != 0 && N < 1920) || (N < 1280 && N % 160 == 0) ||
+                         (N == 1280 && !g_big1280)))
+        continue;
     }
     if (c.bn == 160 && N % 160 != 0) continue;  // the UNet's widths are all multiples of 160
     const long tiles = (long)cdiv(M, c.bm) * cdiv(N, c.bn);
@@ -2720,10 +2792,6 @@ static void launch_cfg(const ConvArgs& a, int ks, bool tapu, int grid, hipStream
 
 // ---- halo-tile 3x3 conv dispatch (conv3x3_halo_kernel)
 static bool g_halo = getenv("LS_HALO") == nullptr || atoi(getenv("LS_HALO")) != 0;  // A/B switch: LS_HALO=0
-// halo pieces over the read pixels only (default since r04k: step -0.5 ms, VAE encode
-// 503 -> 490 ms, decode 529 -> 518 ms per 48-window batch); LS_HALO_RP=0: the padded image
-static bool g_halo_rp = getenv("LS_HALO_RP") == nullptr || atoi(getenv("LS_HALO_RP")) != 0;
-
 // A/B switch (tuning key 13): 128-channel tiles where both divide N (3-slot weight ring
 // instead of 2 at BN 160)
 static bool g_halo_bn128 = getenv("LS_HALO_BN128") != nullptr;
@@ -2750,24 +2818,19 @@ static int halo_tw(const ls_conv_desc* d, const ConvArgs& a) {
   return tw;
 }
 
-template <int TW, int BN, bool GN, bool CSF, bool RP = false>
+template <int TW, int BN, bool GN, bool CSF>
 static void launch_halo3(const ConvArgs& a, hipStream_t s) {
   using HC = HaloCfg<TW, BN>;
   const int grid = a.n_img * (a.H / HC::TH) * (a.W / TW) * (a.N / BN);
-  LS_SET_MAX_DYN_SHM((conv3x3_halo_kernel<TW, BN, GN, CSF, RP>), HC::SHM);
-  conv3x3_halo_kernel<TW, BN, GN, CSF, RP><<<grid, 512, HC::SHM, s>>>(a);
+  LS_SET_MAX_DYN_SHM((conv3x3_halo_kernel<TW, BN, GN, CSF>), HC::SHM);
+  conv3x3_halo_kernel<TW, BN, GN, CSF><<<grid, 512, HC::SHM, s>>>(a);
 }
 
 template <int TW, int BN>
 static void launch_halo2(const ConvArgs& a, hipStream_t s) {
   if (a.aff_scale) {
-    if (g_halo_rp) {
-      if (a.cs_out) launch_halo3<TW, BN, true, true, true>(a, s);
-      else launch_halo3<TW, BN, true, false, true>(a, s);
-    } else {
-      if (a.cs_out) launch_halo3<TW, BN, true, true>(a, s);
-      else launch_halo3<TW, BN, true, false>(a, s);
-    }
+    if (a.cs_out) launch_halo3<TW, BN, true, true>(a, s);
+    else launch_halo3<TW, BN, true, false>(a, s);
   } else {
     if (a.cs_out) launch_halo3<TW, BN, false, true>(a, s);
     else launch_halo3<TW, BN, false, false>(a, s);
@@ -2886,7 +2949,9 @@ extern "C" int ls_set_tuning(int32_t key, int32_t value) {
     case 6: g_rowblock = value != 0; return LS_OK;
     case 7: g_rowblock640 = value != 0; return LS_OK;
     case 8: g_halo = value != 0; return LS_OK;
-    case 12: g_halo_rp = value != 0; return LS_OK;
+    case 12:  // (the padded-row halo image is gone since the compact image, round 5)
+      if (!value) return fail(LS_ERR_INVALID, "LS_HALO_RP=0 (padded halo rows) no longer exists");
+      return LS_OK;
     case 13: g_halo_bn128 = value != 0; return LS_OK;
     case 15: g_rb640_fm2 = value != 0; return LS_OK;
     case 9:

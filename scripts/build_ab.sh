@@ -3,6 +3,7 @@
 # another commit, written to latentsync_amd/libls_hip_ab.so (select it at run time
 # with LS_HIP_LIB=latentsync_amd/libls_hip_ab.so).
 # usage: bash scripts/build_ab.sh COMMIT [csrc file, default ls_gemm.hip]
+#        COMMIT "-" = the working tree's file; EXTRA_FLAGS (env) adds hipcc flags (-DMACRO=...)
 set -e
 commit=$1; file=${2:-ls_gemm.hip}
 root=$(cd "$(dirname "$0")/.." && pwd)
@@ -10,12 +11,12 @@ ab=$root/build/ab
 rm -rf "$ab" && mkdir -p "$ab/latentsync_amd/csrc" "$ab/include"
 cp "$root/include/ls_hip.h" "$ab/include/"
 cp "$root"/latentsync_amd/csrc/* "$ab/latentsync_amd/csrc/"
-git -C "$root" show "$commit:latentsync_amd/csrc/$file" > "$ab/latentsync_amd/csrc/$file"
+[ "$commit" != "-" ] && git -C "$root" show "$commit:latentsync_amd/csrc/$file" > "$ab/latentsync_amd/csrc/$file"
 cd "$ab/latentsync_amd/csrc"
 for f in *.hip; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wno-unused-result -munsafe-fp-atomics \
-    -fno-slp-vectorize -c "$f" -o "${f%.hip}.o" &
+    -fno-slp-vectorize $EXTRA_FLAGS -c "$f" -o "${f%.hip}.o" &
 done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$root/latentsync_amd/libls_hip_ab.so" *.o
-echo "built latentsync_amd/libls_hip_ab.so ($file from $commit)"
+echo "built latentsync_amd/libls_hip_ab.so ($file from $commit, extra flags: ${EXTRA_FLAGS:-none})"

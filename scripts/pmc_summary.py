@@ -22,7 +22,7 @@ def main():
                 per[(did, r["Counter_Name"])] += float(r["Counter_Value"])
                 names[did] = r["Kernel_Name"].split("(")[0][:70]
             for (did, cn), v in per.items():
-                if "conv_gemm" in names[did] or "halo" in names[did] or "rowblock" in names[did] or "attn" in names[did]:
+                if any(k in names[did] for k in ("conv_gemm", "halo", "rowblock", "attn", "ff_fused", "tattn")):
                     groups[(key, names[did])][cn].append(v)
     for (key, kn), cs in sorted(groups.items()):
         print(f"== {key}  {kn}")

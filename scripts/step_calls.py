@@ -40,7 +40,9 @@ def main():
         e.record(torch.cuda.current_stream())
         return e
 
-    names = ["conv", "attention", "group_norm", "group_norm_apply", "row_stats"]
+    names = ["conv", "attention", "group_norm", "group_norm_apply", "row_stats", "layer_norm", "feedforward",
+             "temporal_attention", "cross_attention_block", "small_linear", "ddim_cfg_step", "add_rows"]
+    names = [n for n in names if hasattr(ops, n)]
     orig = {n: getattr(ops, n) for n in names}
 
     def wrap(n):
@@ -48,6 +50,7 @@ def main():
             e0 = ev()
             r = orig[n](*a, **kw)
             e1 = ev()
+            nb = 0.0  # algorithmic HBM bytes (operands once, output once)
             if n == "conv":
                 x, pw = a[0], a[1]
                 x2 = kw.get("x2")
@@ -55,16 +58,41 @@ def main():
                 y = r
                 M = y.shape[0] * y.shape[1] * y.shape[2]
                 fl = 2.0 * M * pw.N * cin * pw.ksize ** 2
+                nb = (x.numel() + (x2.numel() if x2 is not None else 0) + pw.w.numel()) * 2 + y.numel() * y.element_size()
+                if kw.get("res") is not None:
+                    nb += y.numel() * 2
                 key = (n, f"M={M} N={pw.N} K={cin * pw.ksize ** 2} ks={pw.ksize} act={kw.get('act', 0)} "
                           f"res={int(kw.get('res') is not None)} ln={int(kw.get('ln_stats') is not None)} "
-                          f"up={int(kw.get('upsample', False))} s={kw.get('stride', 1)}")
+                          f"aff={int(kw.get('aff') is not None)} up={int(kw.get('upsample', False))} s={kw.get('stride', 1)}")
             elif n == "attention":
                 fl = 4.0 * kw["batch"] * kw["heads"] * kw["nq"] * kw["nk"] * kw["head_dim"]
+                hd = kw["heads"] * kw["head_dim"] * kw["batch"] * 2
+                nb = hd * (2 * kw["nq"] + 2 * kw["nk"])
                 key = (n, f"b={kw['batch']} h={kw['heads']} nq={kw['nq']} nk={kw['nk']} d={kw['head_dim']}")
+            elif n == "feedforward":
+                x2d, w1, w2 = a[0], a[2], a[3]
+                rows, C = x2d.shape
+                fl = 2.0 * rows * w1.N * C + 2.0 * rows * w2.N * (w1.N // 2)
+                nb = rows * C * 2 * 2 + (w1.w.numel() + w2.w.numel()) * 2
+                key = (n, f"rows={rows} C={C} inner={w1.N // 2}")
+            elif n == "temporal_attention":
+                x2d, pk, ns, F, S = a[0], a[1], a[2], a[3], a[4]
+                rows, C = x2d.shape
+                fl = 2.0 * rows * 3 * C * C + 4.0 * ns * S * pk.heads * F * F * (C // pk.heads)
+                nb = rows * C * 2 * 2
+                key = (n, f"rows={rows} C={C} F={F}")
+            elif n == "cross_attention_block":
+                x2d = a[0]
+                rows, C = x2d.shape
+                fl = 4.0 * rows * C * C
+                nb = rows * C * 2 * 2
+                key = (n, f"rows={rows} C={C}")
             else:
                 fl = 0.0
-                key = (n, f"shape={tuple(a[0].shape)}")
-            recs.append((key, e0, e1, fl))
+                t0 = a[0] if hasattr(a[0], "numel") else None
+                nb = 2.0 * t0.numel() * t0.element_size() if t0 is not None else 0.0
+                key = (n, f"shape={tuple(t0.shape) if t0 is not None else ''}")
+            recs.append((key, e0, e1, fl, nb))
             return r
         return f
 
@@ -74,23 +102,30 @@ def main():
     torch.cuda.synchronize()
     for n in names:
         setattr(ops, n, orig[n])
-    agg = collections.defaultdict(lambda: [0, 0.0, 0.0])
+    agg = collections.defaultdict(lambda: [0, 0.0, 0.0, 0.0])
     tot = 0.0
-    for key, e0, e1, fl in recs:
+    for key, e0, e1, fl, nb in recs:
         t = e0.elapsed_time(e1)
         agg[key][0] += 1
         agg[key][1] += t
         agg[key][2] += fl
+        agg[key][3] += nb
         tot += t
     print(f"{phase}: {len(recs)} calls, {tot:.3f} ms summed (windows={nw}, R={R})")
     fam = collections.defaultdict(float)
-    for (n, _), (c, t, fl) in agg.items():
+    for (n, _), (c, t, fl, nb) in agg.items():
         fam[n] += t
     for n, t in sorted(fam.items(), key=lambda x: -x[1]):
-        print(f"  {n:18s} {t:8.3f} ms")
-    for (n, k), (c, t, fl) in sorted(agg.items(), key=lambda x: -x[1][1]):
+        print(f"  {n:22s} {t:8.3f} ms")
+    # excess over a practical roofline: max(flops / 1.6 PF/s, bytes / 6 TB/s)
+    ideal = lambda fl, nb: max(fl / 1.6e15, nb / 6e12) * 1e3
+    print(f"practical roofline (1.6 PF/s MFMA, 6 TB/s HBM): {sum(ideal(v[2], v[3]) for v in agg.values()):.3f} ms "
+          f"of {tot:.3f} ms")
+    for (n, k), (c, t, fl, nb) in sorted(agg.items(), key=lambda x: -(x[1][1] - ideal(x[1][2], x[1][3]))):
         tf = fl / (t * 1e-3) / 1e12 if fl else 0.0
-        print(f"{t:8.3f} ms n={c:3d} avg {t / c * 1e3:8.1f} us {tf:7.1f} TF/s  {n:16s} {k}")
+        gbs = nb / (t * 1e-3) / 1e9
+        print(f"{t:8.3f} ms excess {t - ideal(fl, nb):7.3f} n={c:3d} avg {t / c * 1e3:8.1f} us {tf:7.1f} TF/s "
+              f"{gbs:6.0f} GB/s  {n:16s} {k}")
 
 
 if __name__ == "__main__":
