@@ -182,8 +182,11 @@ __global__ void __launch_bounds__(512, 1) ff_fused_kernel(FFArgs a) {
   }
 }
 
-// ff_pair_kernel (round 5): the same FeedForward with each W fragment read from LDS feeding
-// TWO MFMAs.  ff_fused_kernel's waves own 16 rows, so every 1-KB W1 / W2 fragment it reads
+#ifdef LS_DIAG_KERNELS  // measured and rejected: diagnostics build only
+// ff_pair_kernel (round 5, measured and rejected: 2630 vs 2460 us per call, step +3 ms,
+// profiles/r05g_ff_pair_ab.txt -- the exchange barrier lines every wave up mid-chunk, and the
+// two waves of a SIMD then run their GEMM1 / GELU / GEMM2 phases in step instead of beside
+// each other): the same FeedForward with each W fragment read from LDS feeding TWO MFMAs.  ff_fused_kernel's waves own 16 rows, so every 1-KB W1 / W2 fragment it reads
 // serves one 16x16x32 MFMA: 480 KB of LDS reads per chunk and CU against 1920 MFMA cycles
 // per SIMD, and with the fragment-read -> MFMA dependency neither the matrix pipe (38 %
 // busy) nor the LDS (40 %) is kept full (PMC, profiles/r05d_ff_pmc.txt).  Here a PAIR of
@@ -367,6 +370,8 @@ __global__ void __launch_bounds__(512, 1) ff_pair_kernel(FFArgs a) {
   }
 }
 
+#endif  // LS_DIAG_KERNELS
+
 }  // namespace ls
 
 using namespace ls;
@@ -385,13 +390,15 @@ extern "C" int ls_feedforward(const ls_ff_desc* d, void* stream) {
   a.x = (const u16*)d->x; a.ln_mr = d->ln_rowstats; a.w1 = (const u16*)d->w1; a.b1 = d->b1;
   a.w2 = (const u16*)d->w2; a.b2 = d->b2; a.y = (u16*)d->y; a.M = d->M; a.ldx = d->ldx; a.ldy = d->ldy;
   constexpr int C = 320, I = 1280;
-  static const bool v1 = getenv("LS_FF_V1") != nullptr && atoi(getenv("LS_FF_V1")) != 0;  // A/B switch
-  if (!v1) {
+#ifdef LS_DIAG_KERNELS
+  static const bool pair = getenv("LS_FF_PAIR") != nullptr && atoi(getenv("LS_FF_PAIR")) != 0;  // A/B switch
+  if (pair) {
     const size_t shm = (size_t)2 * (64 * (C / 64) * 8 + C * 4) * 16 + 2 * I * sizeof(float) + 4 * 2 * 2 * 64 * 8;
     LS_SET_MAX_DYN_SHM((ff_pair_kernel<C, I>), (int)shm);
     ff_pair_kernel<C, I><<<(unsigned)((d->M + 127) / 128), 512, shm, (hipStream_t)stream>>>(a);
     return check_launch("ff_pair_kernel");
   }
+#endif
   const size_t shm = (size_t)2 * (64 * (C / 64) * 8 + C * 4) * 16 + 2 * I * sizeof(float);
   LS_SET_MAX_DYN_SHM((ff_fused_kernel<C, I>), (int)shm);
   ff_fused_kernel<C, I><<<(unsigned)((d->M + 127) / 128), 512, shm, (hipStream_t)stream>>>(a);
