@@ -2191,7 +2191,8 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
 // outweighs the MFMAs it feeds (the VAE's 128-channel convs at 256^2 ran at 0.34 of the
 // bf16 peak), and a GroupNorm affine + SiLU on the input had to be materialised by its
 // own pass (ls_groupnorm_apply) because applying it in the gather would repeat it 9 times.
-// Here a block owns a TH x TW patch of one image (256 output pixels) x BN output channels:
+// Here a block owns a TH x TW patch of one image (256 output pixels; 128 in the 16 x 8
+// form below) x BN output channels:
 //   * per 64-channel chunk, the (TH + 2) x (TW + 2) input pixels of the patch are loaded
 //     ONCE (buffer loads into registers; pixels outside the image read zeros), optionally
 //     put through y = silu?(x * scale + shift) (the GroupNorm affine of the pixel's sample)
@@ -2200,11 +2201,11 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
 //     the 9 taps need (brute-forced over the lane groups; the GEMMs' ((row >> 1) & 7)
 //     swizzle is 2-way there).  Halo rows are TW + 8 pixels long (== 0 mod 8), so the
 //     swizzle phase of every fragment of a wave equals its first fragment's: one address
-//     computation per (tap, k-step) and lane, fragment offsets are immediates (round 5
-//     measured the compact TW + 2 row with a column-based swizzle: it frees 28 KB of LDS,
-//     but the third weight slot at BN 160 that room was for spills 30 VGPRs, so not kept);
+//     computation per (tap, k-step) and lane, fragment offsets are immediates (the compact
+//     TW + 2 row with a column-based swizzle frees 28 KB of LDS, but the third weight slot
+//     at BN 160 that room was for spills 30 VGPRs; the 16 x 8 form uses it to fit 2 blocks);
 //   * the 9 taps of the chunk then run from that image: tap (kh, kw) shifts the read by
-//     kh (TW + 8) + kw pixels; the weight K-tile of each tap ([BN][64], channel-chunk-major
+//     kh P + kw pixels (P the row pitch); the weight K-tile of each tap ([BN][64], channel-chunk-major
 //     packing) streams through an NSW-slot LDS ring by LDS-DMA, NSW - 1 taps ahead;
 //   * the halo of chunk c + 1 is loaded into registers at tap 0 of chunk c and written to
 //     the other halo image at tap 8 (so the input affine's VALU work overlaps the MFMAs
@@ -2212,19 +2213,29 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
 // 8 waves as 4 (pixels) x 2 (channels), 64 x BN/2 per wave; the epilogue is
 // store_tile_plain (bias, per-frame row vector, residual, scale, GroupNorm column sums
 // of the output) with the patch's rows mapped back to image rows.
-template <int TW, int BN>
+// TH = 256 / TW: 16 x 16 patches, 8 waves, one block per CU (the shipped UNet form).
+// TH = 8 (round 5, BN 128: the VAE's convs): 16 x 8 patches, 4 waves as 2 (pixels) x 2
+// (channels), compact halo rows (TW + 2 pixels, chunks swizzled by the halo COLUMN & 7 --
+// conflict-free at any row / column offset, brute-forced -- so fragments one patch row
+// apart still share the swizzle phase) and a 2-slot weight ring: 80 KB of LDS, TWO blocks
+// per CU, so one block's halo prologue, chunk transitions and epilogue overlap the other's
+// MFMAs (the 1-block form waited 44.5 % of its wave time, profiles/r05a_h128_summary.txt).
+template <int TW, int BN, int TH_ = 256 / TW>
 struct HaloCfg {
-  static constexpr int TH = 256 / TW;
-  static constexpr int P = TW + 8;                       // halo row pitch (pixels), 0 mod 8
+  static constexpr int TH = TH_;
+  static constexpr int NT = (TH / 4) * 2 * 64;           // threads: (TH / 4) pixel waves x 2 channel waves
+  static constexpr bool COMPACT = TH < 16;
+  static constexpr int P = COMPACT ? TW + 2 : TW + 8;    // halo row pitch (pixels); padded: 0 mod 8
   static constexpr int HALO = (TH + 2) * P * 8;          // uint4 per halo image
   static constexpr int WSLOT = BN * 8;                   // uint4 per weight ring slot (BN x 64 k)
-  static constexpr int NSW = BN <= 128 ? 3 : 2;          // weight ring slots (3 at BN 160: 30 VGPRs of spills)
-  static constexpr int NHL = (HALO + 511) / 512;         // halo loads per thread per chunk
-  static constexpr int DPT = (WSLOT + 511) / 512;        // weight DMAs per thread per tap
+  // weight ring slots (3 at BN 160 spills 30 VGPRs; the 2-block form has LDS for 2)
+  static constexpr int NSW = COMPACT ? 2 : BN <= 128 ? 3 : 2;
+  static constexpr int DPT = (WSLOT + NT - 1) / NT;      // weight DMAs per thread per tap
   static constexpr int FN = BN / 32;                     // 16-column fragments per wave
   static constexpr size_t SHM = ((size_t)2 * HALO + (size_t)NSW * WSLOT + 64 + 64) * 16;  // + dummy, affine
-  static_assert(SHM <= 163840, "halo conv LDS");
-  static_assert((size_t)64 * (BN + 4) * 4 <= (size_t)HALO * 16, "epilogue staging fits one halo image");
+  static_assert(SHM <= (COMPACT ? 81920 : 163840), "halo conv LDS (compact: two blocks per CU)");
+  static_assert((size_t)64 * (BN + 4) * 4 <= (size_t)2 * HALO * 16, "epilogue staging fits the halo images");
+  static_assert(TW == 16 && (TH == 16 || TH == 8), "16-pixel patch rows, 16 or 8 of them");
 };
 
 
@@ -2241,12 +2252,14 @@ __host__ __device__ constexpr int halo_issue(int t, int nhl, bool gn) {
 
 // Halo pieces: the (TH + 2) x (TW + 2) pixels the taps read x 8 16-B chunks (2592 pieces at
 // 16 x 16: 5.06 per thread); piece j of a thread has its own LDS slot hdst[j].
-template <int TW, int BN, bool GN, bool CSF>
-__global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
-  using HC = HaloCfg<TW, BN>;
-  constexpr int TH = HC::TH, P = HC::P, HALO = HC::HALO, WSLOT = HC::WSLOT, NSW = HC::NSW;
+template <int TW, int BN, bool GN, bool CSF, int TH_ = 256 / TW>
+__global__ void __launch_bounds__(TH_ / 4 * 128, 16 / TH_) conv3x3_halo_kernel(ConvArgs a) {
+  using HC = HaloCfg<TW, BN, TH_>;
+  constexpr int TH = HC::TH, P = HC::P, HALO = HC::HALO, WSLOT = HC::WSLOT, NSW = HC::NSW, NT = HC::NT;
+  constexpr bool COMPACT = HC::COMPACT;
+  static_assert(NT == TH_ / 4 * 128, "launch bounds");
   constexpr int NPC = (TH + 2) * (TW + 2) * 8;  // pieces per chunk (the read pixels)
-  constexpr int NHL = (NPC + 511) / 512, DPT = HC::DPT, FM = 4, FN = HC::FN, WTN = BN / 2;
+  constexpr int NHL = (NPC + NT - 1) / NT, DPT = HC::DPT, FM = 4, FN = HC::FN, WTN = BN / 2;
   constexpr int HB = (NHL + 2) / 3;  // largest batch
   extern __shared__ __attribute__((aligned(16))) uint4 lds_dyn[];
   uint4* const hbuf = lds_dyn;                 // [2][HALO]
@@ -2270,19 +2283,24 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
   const int nchunk = a.Cin / 64;
   const int G = 9 * nchunk;  // taps in all
 
-  // ---- this thread's halo pieces: q = j*512 + tid -> read pixel q / 8 (row-major over the
+  // ---- this thread's halo pieces: q = j*NT + tid -> read pixel q / 8 (row-major over the
   // (TH + 2) x (TW + 2) pixels the taps read), logical 16-B chunk tid & 7; its slot in the
-  // padded image: row hr, column hcol + 3, the chunk swizzled by (slot & 7)
+  // padded image: row hr, column hcol + 3, the chunk swizzled by (slot & 7); compact: row
+  // hr, column hcol, swizzled by (hcol & 7)
   const int hc8 = tid & 7;
   int hpix[NHL];  // pixel index within the image, or -1 (outside: zeros)
   int hdst[NHL];
 #pragma unroll
   for (int j = 0; j < NHL; ++j) {
-    const int q = j * 512 + tid, hp = q >> 3;
+    const int q = j * NT + tid, hp = q >> 3;
     const int hr = hp / (TW + 2), hcol = hp - hr * (TW + 2);
     const int y = y0 - 1 + hr, x = x0 - 1 + hcol;
-    const int slot = hr * P + hcol + 3;
-    hdst[j] = slot * 8 + (hc8 ^ (slot & 7));
+    if constexpr (COMPACT) {  // row hr, column hcol, the chunk swizzled by the column
+      hdst[j] = (hr * P + hcol) * 8 + (hc8 ^ (hcol & 7));
+    } else {
+      const int slot = hr * P + hcol + 3;
+      hdst[j] = slot * 8 + (hc8 ^ (slot & 7));
+    }
     hpix[j] = q < NPC && y >= 0 && y < a.H && x >= 0 && x < a.W ? y * a.W + x : -1;
   }
   const uint32_t cap = 0x7FFFFFFFu;
@@ -2325,7 +2343,7 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
     }
 #pragma unroll
     for (int j = j0; j < j1; ++j) {
-      if (j * 512 + tid >= NPC) continue;
+      if (j * NT + tid >= NPC) continue;
       uint4 v = hreg[j - j0];
       if constexpr (GN) {
         if (hpix[j] >= 0) {  // zero padding stays zero: the conv pads the ACTIVATED input
@@ -2349,7 +2367,7 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
   int wvo[DPT];
 #pragma unroll
   for (int j = 0; j < DPT; ++j) {
-    const int q = j * 512 + tid, row = q >> 3, pc = q & 7;
+    const int q = j * NT + tid, row = q >> 3, pc = q & 7;
     const int lc = pc ^ ((row >> 1) & 7);
     wvo[j] = ((q < WSLOT ? row : 0) * a.K + lc * 8) * 2;
   }
@@ -2360,8 +2378,8 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
     uint4* slot = wbuf + sl * WSLOT;
 #pragma unroll
     for (int j = 0; j < DPT; ++j) {
-      const bool live = j * 512 + wid_u * 64 < WSLOT;  // wave-uniform
-      ls_raw_buffer_load_lds(rs_w, (__attribute__((address_space(3))) void*)(live ? slot + j * 512 + wid_u * 64 : dummy),
+      const bool live = j * NT + wid_u * 64 < WSLOT;  // wave-uniform
+      ls_raw_buffer_load_lds(rs_w, (__attribute__((address_space(3))) void*)(live ? slot + j * NT + wid_u * 64 : dummy),
                              16, wvo[j], g * 128, 0, 0);
     }
   };
@@ -2370,7 +2388,7 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
   // fragment i is patch row 4 wm + i, column l16)
   static_assert(TW == 16, "fragment i = one patch row");
   const int p0 = 64 * wm + l16;
-  const int hp0 = (p0 / TW) * P + (p0 % TW) + 3;  // halo pixel of fragment 0 at tap (0, 0)
+  const int hp0 = (p0 / TW) * P + (p0 % TW) + (COMPACT ? 0 : 3);  // halo pixel of fragment 0 at tap (0, 0)
 
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -2394,7 +2412,9 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
   bf16x8 apf[2][FM];  // A fragments of the current tap (both k-steps)
   auto read_a = [&](const uint4* hb, int tt) {  // (tt compile-time after inlining)
     const int hpt = hp0 + (tt / 3) * P + tt % 3;
-    const int sw = hpt & 7;  // (P == 0 mod 8: the phase of every fragment of the wave)
+    // the swizzle phase, shared by the wave's fragments: padded rows (P == 0 mod 8) the
+    // pixel's, compact rows the halo column's (l16 + kw)
+    const int sw = COMPACT ? (l16 + tt % 3) & 7 : hpt & 7;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int base = hpt * 8 + ((ks * 4 + lg) ^ sw);
@@ -2460,9 +2480,9 @@ __global__ void __launch_bounds__(512) conv3x3_halo_kernel(ConvArgs a) {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   // epilogue: virtual rows (GroupNorm slots) = the patch's index within its image x 256
-  const int m0v = (int)(img * HW) + (tyb * tpr + txb) * 256;
+  const int m0v = (int)(img * HW) + (tyb * tpr + txb) * (TH * TW);
   const long m0r = img * HW + (long)y0 * a.W + x0;
-  store_tile_plain<256, BN, 4, 2, false, CSF, TW>(a, acc, (float*)lds_dyn, m0v, n0, m0r);
+  store_tile_plain<TH * TW, BN, TH / 4, 2, false, CSF, TW>(a, acc, (float*)lds_dyn, m0v, n0, m0r);
 }
 
 // ---------------------------------------------------------------- host side
@@ -2818,28 +2838,36 @@ static int halo_tw(const ls_conv_desc* d, const ConvArgs& a) {
   return tw;
 }
 
-template <int TW, int BN, bool GN, bool CSF>
+template <int TW, int BN, bool GN, bool CSF, int TH>
 static void launch_halo3(const ConvArgs& a, hipStream_t s) {
-  using HC = HaloCfg<TW, BN>;
+  using HC = HaloCfg<TW, BN, TH>;
   const int grid = a.n_img * (a.H / HC::TH) * (a.W / TW) * (a.N / BN);
-  LS_SET_MAX_DYN_SHM((conv3x3_halo_kernel<TW, BN, GN, CSF>), HC::SHM);
-  conv3x3_halo_kernel<TW, BN, GN, CSF><<<grid, 512, HC::SHM, s>>>(a);
+  LS_SET_MAX_DYN_SHM((conv3x3_halo_kernel<TW, BN, GN, CSF, TH>), HC::SHM);
+  conv3x3_halo_kernel<TW, BN, GN, CSF, TH><<<grid, HC::NT, HC::SHM, s>>>(a);
 }
 
-template <int TW, int BN>
+template <int TW, int BN, int TH = 256 / TW>
 static void launch_halo2(const ConvArgs& a, hipStream_t s) {
   if (a.aff_scale) {
-    if (a.cs_out) launch_halo3<TW, BN, true, true>(a, s);
-    else launch_halo3<TW, BN, true, false>(a, s);
+    if (a.cs_out) launch_halo3<TW, BN, true, true, TH>(a, s);
+    else launch_halo3<TW, BN, true, false, TH>(a, s);
   } else {
-    if (a.cs_out) launch_halo3<TW, BN, false, true>(a, s);
-    else launch_halo3<TW, BN, false, false>(a, s);
+    if (a.cs_out) launch_halo3<TW, BN, false, true, TH>(a, s);
+    else launch_halo3<TW, BN, false, false, TH>(a, s);
   }
 }
+
+// 16 x 8 patches, two blocks per CU for the 128-column tiles of convs with at most 4 input
+// chunks (Cin <= 256), where a block's halo prologue and epilogue are a large share of its
+// time: VAE 128 ch at 256^2 17.67 -> 17.23 ms, 128 -> 256 at 128^2 8.74 -> 8.43 ms, 256 at
+// 128^2 a tie; at Cin 512 (8 chunks) the 2-slot weight ring loses to the 1-block form's 3
+// slots (13.12 -> 13.55 ms at 64^2), profiles/r05k_halo_ab.txt.  A/B switch LS_HALO_TH8=0.
+static bool g_halo_th8 = getenv("LS_HALO_TH8") == nullptr || atoi(getenv("LS_HALO_TH8")) != 0;
 
 template <int TW>
 static void launch_halo1(const ConvArgs& a, hipStream_t s) {
   if (a.N % 160 == 0 && !(g_halo_bn128 && a.N % 128 == 0)) launch_halo2<TW, 160>(a, s);
+  else if (g_halo_th8 && a.H % 8 == 0 && a.Cin <= 256) launch_halo2<TW, 128, 8>(a, s);
   else launch_halo2<TW, 128>(a, s);
 }
 
@@ -2954,6 +2982,7 @@ extern "C" int ls_set_tuning(int32_t key, int32_t value) {
       return LS_OK;
     case 13: g_halo_bn128 = value != 0; return LS_OK;
     case 15: g_rb640_fm2 = value != 0; return LS_OK;
+    case 16: g_halo_th8 = value != 0; return LS_OK;
     case 9:
 #ifndef LS_DIAG_KERNELS
       if (value) return fail(LS_ERR_INVALID, "attn6: diagnostics build only");

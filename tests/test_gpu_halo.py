@@ -1,4 +1,4 @@
-"""The halo-tile 3x3 conv (conv3x3_halo_kernel, ls_conv_path 3): a 16 x 16 patch of
+"""The halo-tile 3x3 conv (conv3x3_halo_kernel, ls_conv_path 3): a 16 x 16 (128-column tiles: 16 x 8) patch of
 output pixels per block, its (16 + 2)^2 input pixels loaded once per 64-channel chunk
 into LDS and put through the GroupNorm affine + SiLU there (resnet.py:185-213 /
 diffusers ResnetBlock2D: conv(silu(GN(x)))), the 9 taps read from that image.  Checked
@@ -31,8 +31,21 @@ def _bf(t):
     (2, 32, 32, 512, 0, 512, 1, True, False, False),     # VAE 512 ch (BN 128, 8 chunks)
     (3, 48, 16, 64, 0, 256, 3, True, False, False),      # one 64-channel chunk, non-square
 ])
-def test_halo_conv(gpu, n, H, W, C1, C2, N, ipp, aff, rowvec, res):
+@pytest.mark.parametrize("th8", [1, 0])
+def test_halo_conv(gpu, n, H, W, C1, C2, N, ipp, aff, rowvec, res, th8):
+    """th8: 128-column tiles (Cin <= 256) on 16 x 8 patches, two blocks per CU (tuning key 16, the
+    default) or on the 16 x 16 one-block form; 160-column tiles are 16 x 16 either way."""
     lib = _lib.load()
+    if N % 160 == 0 and not th8:
+        pytest.skip("160-column tiles have one patch form")
+    assert lib.ls_set_tuning(16, th8) == 0
+    try:
+        _halo_case(lib, n, H, W, C1, C2, N, ipp, aff, rowvec, res)
+    finally:
+        lib.ls_set_tuning(16, 1)
+
+
+def _halo_case(lib, n, H, W, C1, C2, N, ipp, aff, rowvec, res):
     g = torch.Generator().manual_seed(n * 1000 + H + C1 + C2 + N)
     Cin = C1 + C2
     x = _bf(torch.randn(n, H, W, C1, generator=g) * 2 + 0.5)
