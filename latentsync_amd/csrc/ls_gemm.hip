@@ -1908,7 +1908,14 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
   // images, then the chunk's 64 bias, colsum and row-vector values (wave 0).
   // piece q = p * 512 + tid of a chunk's images: image t = q / (8 BN), row (q / 8) % BN, chunk q % 8
   const long rv_base = RV ? rv_row(a, rb * BM) : 0;  // host: rows_per_vec % BM == 0
+#ifdef LS_DIAG_KERNELS  // timing ablations (LS_GEMM_ABLATE): 2 no chunk DMA past the first two, 4 no
+  // stores, 64 no A-row loads (zeros) -- results are garbage; profiles/r05l_ablate.txt
+  const int abl = a.ablate;
+#else
+  constexpr int abl = 0;
+#endif
   auto issue = [&](int c, int stage) {
+    if ((abl & 2) && c > c0 + 1) return;
     uint4* dst = lds_dyn + stage * STAGE;
 #pragma unroll
     for (int p = 0; p < PPT; ++p) {
@@ -1943,7 +1950,7 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
   for (int i = 0; i < FM; ++i) {
     const u16* src = a.x1 + (long)(mw + i * 16 + l16) * a.ld1 + lg * 8;
 #pragma unroll
-    for (int s = 0; s < KT; ++s) ar[i][s] = *(const bf16x8*)(src + s * 32);
+    for (int s = 0; s < KT; ++s) ar[i][s] = (abl & 64) ? bf16x8{} : *(const bf16x8*)(src + s * 32);
   }
   if (LN) {
     // LayerNorm applied to the register-resident A rows once ((x - mean) * rstd, rounded
@@ -2045,7 +2052,7 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
             for (int r = 0; r < 4; ++r) o[r] = (acc[i][j][r] + r4[r]) * a.out_scale;
           }
           const uint2 pk = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
-          *(uint2*)(yrow + nb + 16 * j) = pk;
+          if (!(abl & 4) || pk.x == 0x12345u) *(uint2*)(yrow + nb + 16 * j) = pk;
           if (CS) {
             gcs[i][j][0] = __uint_as_float(pk.x << 16); gcs[i][j][1] = __uint_as_float(pk.x & 0xffff0000u);
             gcs[i][j][2] = __uint_as_float(pk.y << 16); gcs[i][j][3] = __uint_as_float(pk.y & 0xffff0000u);
