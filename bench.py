@@ -31,6 +31,7 @@ import os
 import socket
 import subprocess
 import sys
+import threading
 import time
 import traceback
 
@@ -294,11 +295,26 @@ def cpu_baseline(unet, vae, R=256, steps=20, guidance=1.0, sample_steps=None):
     n = steps if sample_steps is None else min(sample_steps, steps)
 
     def window(k):
-        with torch.no_grad():
-            t0 = time.perf_counter()
-            O.pipeline_window(usd, dict(unet.config), vsd, faces, mask, audio, init, em, er, num_steps=k,
-                              guidance_scale=guidance)
-            return time.perf_counter() - t0
+        # a progress line on stderr every 60 s: an oracle window at 512^2 runs for minutes
+        # without output, which a supervisor watching the output would take for a hang
+        done = threading.Event()
+
+        def beat():
+            t_b = time.perf_counter()
+            while not done.wait(60.0):
+                print(f"cpu_baseline: oracle window ({k} DDIM steps) running, {time.perf_counter() - t_b:.0f} s",
+                      file=sys.stderr, flush=True)
+        hb = threading.Thread(target=beat, daemon=True)
+        hb.start()
+        try:
+            with torch.no_grad():
+                t0 = time.perf_counter()
+                O.pipeline_window(usd, dict(unet.config), vsd, faces, mask, audio, init, em, er, num_steps=k,
+                                  guidance_scale=guidance)
+                return time.perf_counter() - t0
+        finally:
+            done.set()
+            hb.join()
     t = window(n)
     if n == steps:
         sample = (f"one full {R}x{R} 16-frame window, {steps} DDIM steps, guidance {guidance}: VAE enc x2 + "
