@@ -1879,7 +1879,7 @@ using namespace ls;
 static bool g_attn_v1 = getenv("LS_ATTN_V1") != nullptr;  // A/B switch: force the 16-query kernel
 static bool g_attn_v3 = getenv("LS_ATTN_V3") != nullptr;  // A/B switch: attn3 for d = 40 too
 // A/B switch: d = 40 self attention on attn6 (32x32x16); measured 3 % slower than attn5 at 48
-// windows (1670 vs 1620 us per call, profiles/r04b_attn_ab.txt), so attn5 stays the default
+// windows (1670 vs 1620 us per call, profiles/r04b_attn6_vs_attn5_ab.txt), so attn5 stays the default
 #ifdef LS_DIAG_KERNELS
 static bool g_attn6 = getenv("LS_ATTN6") != nullptr;
 #else

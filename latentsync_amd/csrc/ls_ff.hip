@@ -184,7 +184,7 @@ __global__ void __launch_bounds__(512, 1) ff_fused_kernel(FFArgs a) {
 
 #ifdef LS_DIAG_KERNELS  // measured and rejected: diagnostics build only
 // ff_pair_kernel (round 5, measured and rejected: 2630 vs 2460 us per call, step +3 ms,
-// profiles/r05g_ff_pair_ab.txt -- the exchange barrier lines every wave up mid-chunk, and the
+// profiles/r05g_ff.txt, r05g_step_ab.txt -- the exchange barrier lines every wave up mid-chunk, and the
 // two waves of a SIMD then run their GEMM1 / GELU / GEMM2 phases in step instead of beside
 // each other): the same FeedForward with each W fragment read from LDS feeding TWO MFMAs.  ff_fused_kernel's waves own 16 rows, so every 1-KB W1 / W2 fragment it reads
 // serves one 16x16x32 MFMA: 480 KB of LDS reads per chunk and CU against 1920 MFMA cycles

@@ -42,7 +42,7 @@ struct ConvArgs {
 // tiles per group, the row-block index fastest.  Tiles running together on an XCD (xcd_remap
 // gives every XCD a contiguous logical range) then share gm A row-bands and ~(concurrent /
 // gm) W column panels instead of one A band and a W panel per tile: the wide linears
-// (GEGLU W1, fused q|k|v) re-fetched their whole W per row-band (profiles/r03e_per_kernel.txt).
+// (GEGLU W1, fused q|k|v) re-fetched their whole W per row-band (profiles/r03e_pmc_per_kernel.txt).
 // gm = 1 is the plain column-fastest order.
 __device__ __forceinline__ void tile_of(const ConvArgs& a, int bid, int& tm, int& tn) {
   const int gsz = a.gm * a.ntn, g = bid / gsz, r = bid - g * gsz;
@@ -55,7 +55,7 @@ __device__ __forceinline__ void tile_of(const ConvArgs& a, int bid, int& tm, int
 // ci % 64 -- the 9 taps of one 64-channel chunk are consecutive K-tiles, so a block reads
 // a pixel chunk's 3x3 neighbourhood in 9 back-to-back K-tiles and the re-reads hit L2
 // (tap-major, the 9 re-reads of a pixel were Cin / 64 K-tiles apart and, with 64 blocks
-// per XCD streaming operands in between, missed: profiles/r03e_per_kernel.txt).
+// per XCD streaming operands in between, missed: profiles/r03e_pmc_per_kernel.txt).
 // Returns the tap and sets c0 = the K-tile's first input channel (k0 = a 64-aligned or,
 // for BK 32, 32-aligned K offset).
 __device__ __forceinline__ int tap_of(const ConvArgs& a, int k0, int& c0) {
