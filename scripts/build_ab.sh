@@ -13,10 +13,12 @@ cp "$root/include/ls_hip.h" "$ab/include/"
 cp "$root"/latentsync_amd/csrc/* "$ab/latentsync_amd/csrc/"
 [ "$commit" != "-" ] && git -C "$root" show "$commit:latentsync_amd/csrc/$file" > "$ab/latentsync_amd/csrc/$file"
 cd "$ab/latentsync_amd/csrc"
+pids=()
 for f in *.hip; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wno-unused-result -munsafe-fp-atomics \
     -fno-slp-vectorize $EXTRA_FLAGS -c "$f" -o "${f%.hip}.o" &
+  pids+=($!)
 done
-wait
+for p in "${pids[@]}"; do wait "$p" || { echo "a compile failed"; exit 1; }; done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$root/latentsync_amd/libls_hip_ab.so" *.o
 echo "built latentsync_amd/libls_hip_ab.so ($file from $commit, extra flags: ${EXTRA_FLAGS:-none})"

@@ -8,11 +8,13 @@ root=$(cd "$(dirname "$0")/.." && pwd)
 ab=$root/build/ab_$tag
 rm -rf "$ab" && mkdir -p "$ab"
 cd "$root/latentsync_amd/csrc"
+pids=()
 for f in *.hip; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wno-unused-result -munsafe-fp-atomics \
     -fno-slp-vectorize $flags -Rpass-analysis=kernel-resource-usage -c "$f" -o "$ab/${f%.hip}.o" 2> "$ab/${f%.hip}.rem" &
+  pids+=($!)
 done
-wait
+for p in "${pids[@]}"; do wait "$p" || { echo "a compile failed (see $ab/*.rem)"; exit 1; }; done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$root/latentsync_amd/libls_hip_$tag.so" "$ab"/*.o
 python3 - "$ab" <<'PY'
 import glob, re, sys
