@@ -2497,6 +2497,7 @@ static bool g_force_regstage = getenv("LS_GEMM_REGSTAGE") != nullptr;
 // A/B switch: 3x3 weights packed tap-major (packing.py reads the same variable)
 static const bool g_w3_tapmajor = getenv("LS_W3_TAPMAJOR") != nullptr;
 static const int g_gemm_gm = getenv("LS_GEMM_GM") ? atoi(getenv("LS_GEMM_GM")) : 0;  // A/B switch: tile raster
+static const bool g_gm_shortk = getenv("LS_GEMM_GM_SHORTK") == nullptr || atoi(getenv("LS_GEMM_GM_SHORTK")) != 0;
 static int g_force_tile = 0, g_force_split = 0, g_bk = 64;
 // ablation bits (diagnostics; tuning key 4 or LS_GEMM_ABLATE): 1 no MFMA, 2 no operand DMA,
 // 4 no output store, 8 the general epilogue arithmetic even where the short path applies
@@ -2950,6 +2951,10 @@ static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split
   // against the column-fastest order over three alternated same-box rounds
   // (profiles/r03i_locality_sweep.txt), so the default stays column-fastest (gm = 1)
   a.gm = g_gemm_gm > 0 ? g_gemm_gm : 1;
+  // round 5: 4 row bands per group for 256x256 1x1 tiles with K <= 1920 (out2 181 -> 173 us,
+  // sc2b -1 %, profiles/r05s_gm_ab.txt; at K = 5120 the grouping loses); A/B switch
+  // LS_GEMM_GM_SHORTK=0
+  if (g_gemm_gm <= 0 && g_gm_shortk && t.bm == 256 && t.bn == 256 && d->ksize == 1 && d->K <= 1920) a.gm = 4;
   a.gm = std::max(1, std::min(a.gm, a.ntm));
   split = d->split_k > 0 ? d->split_k : t.split;
   split = std::min(split, a.ktiles);
