@@ -14,11 +14,14 @@ directly spawns N fresh worker processes of this script (RANK / LOCAL_RANK /
 WORLD_SIZE / MASTER_* in their environment) BEFORE anything touches the GPU and
 exits with the first failing worker's status; under torchrun the process is
 already a worker.  Every rank runs its own windows (weak scaling; rank r owns
-windows r, r+N, ... of the job) and the decoded frames of all ranks are
-all-gathered once at the end of the timed loop as the fp32 pasted frames
-LipsyncPipeline.run_windows exchanges (RCCL over xGMI, the only collective; the
-uint8 clip is derived after it; the process group carries a timeout so a dead
-rank aborts the gather instead of hanging it).  `n_gpus` is the world size the process group
+the contiguous block of K*nw windows [r*K*nw, (r+1)*K*nw) of the job) and the
+decoded frames of all ranks are all-gathered once at the end of the timed loop as
+the fp32 pasted frames LipsyncPipeline.run_windows exchanges (RCCL over xGMI, the
+only collective; the receive buffer is already in clip order, and the uint8 clip
+is derived from it in bounded chunks; the process group carries a timeout so a
+dead rank aborts the gather instead of hanging it).  The per-rank memory of that
+exchange is `exchange_bytes` (K = 20, 48 windows, 8 ranks: 133 GB beside the
+engine); the line reports the measured peak (`peak_hbm_gb`).  `n_gpus` is the world size the process group
 reports.  Rank 0 prints ONE JSON line.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1|2|4]
@@ -376,8 +379,9 @@ class PlumbingEngine:
     the GPU bench, with the window's compute replaced by writing the global window
     index into its frames so the gathered clip order can be checked."""
 
-    def __init__(self, F, R, nw, rank, world):
+    def __init__(self, F, R, nw, rank, world, owned):
         self.F, self.R, self.nw, self.rank, self.world = F, R, nw, rank, world
+        self.owned = owned  # global indices of this rank's windows, in run order
         self.out = torch.zeros((nw * F, 3, R, R), dtype=torch.float32)
         self.calls = 0
 
@@ -385,9 +389,22 @@ class PlumbingEngine:
         for k in range(self.nw):
             local = self.calls * self.nw + k
             # window index w encoded as the pasted value whose uint8 is w % 251
-            w = (self.rank + local * self.world) % 251
+            w = self.owned[local % len(self.owned)] % 251
             self.out[k * self.F:(k + 1) * self.F] = (w + 0.5) / 255 * 2 - 1
         self.calls += 1
+
+
+def exchange_bytes(world, K, nw, F=16, R=256):
+    """Per-rank memory of the end-of-loop exchange (beyond the engine): this rank's
+    fp32 pasted frames (K*nw windows), the all-gather's receive buffer (world*K*nw
+    windows, shard.gather_bytes; none at world 1), the uint8 clip of every window and
+    frames_to_u8's two chunk temporaries."""
+    from latentsync_amd import shard
+    from latentsync_amd.pipeline import U8_CHUNK
+    win32 = F * 3 * R * R * 4
+    n = world * K * nw
+    return (K * nw * win32 + shard.gather_bytes(n, world, win32) + n * F * R * R * 3
+            + 2 * U8_CHUNK * 3 * R * R * 4)
 
 
 def free_port():
@@ -448,8 +465,11 @@ def worker(args):
     F, R = 16, args.resolution
     h = R // 8
     nw = args.windows_per_batch
+    K, W = args.steps, args.warmup
+    # rank r owns the contiguous block of K*nw windows of the job (shard.rank_windows)
+    owned = shard.rank_windows(world * K * nw, world, rank)
     if plumbing:
-        eng = PlumbingEngine(F, R, nw, rank, world)
+        eng = PlumbingEngine(F, R, nw, rank, world, owned)
         unet = vae = None
     else:
         from latentsync_amd.config import STAGE2_MODEL
@@ -472,15 +492,14 @@ def worker(args):
         if not plumbing:
             torch.cuda.synchronize(device)
 
-    K, W = args.steps, args.warmup
     FB = F * nw  # frames per step (batch of windows)
-    # rank r owns windows r, r+N, ... of the job (shard.rank_windows); K*nw per rank,
-    # kept as the fp32 pasted frames LipsyncPipeline.run_windows gathers
-    mine = torch.empty((K * nw, F, 3, R, R), dtype=torch.float32, device=device)
+    # this rank's K*nw windows, kept as the fp32 pasted frames LipsyncPipeline.run_windows gathers
+    mine = torch.empty((len(owned), F, 3, R, R), dtype=torch.float32, device=device)
     for _ in range(max(W, 1) if not (args.no_graphs or plumbing) else W):
         eng.run()
     if plumbing:
         eng.calls = 0
+    engine_bytes = None if plumbing else torch.cuda.max_memory_allocated(device)
     if args.fail_rank == rank:
         raise RuntimeError(f"injected failure on rank {rank} (--fail-rank)")
     if args.stall_rank == rank:
@@ -502,9 +521,11 @@ def worker(args):
             ev_step.append((e0, e1))
         mine[k * nw:(k + 1) * nw].copy_(eng.out.view(nw, F, 3, R, R))
     # decoded frames of every rank back in clip order: ONE all-gather over xGMI, at the
-    # end, then the uint8 clip -- exactly LipsyncPipeline.run_windows' exchange
-    gathered = frames_to_u8(shard.gather_windows(mine, world * K * nw).flatten(0, 1))
-    gathered = gathered.view(world * K * nw, F, R, R, 3)
+    # end, into a receive buffer that is already clip order, then the uint8 clip in
+    # bounded chunks -- exactly LipsyncPipeline.run_windows' exchange
+    clip = shard.gather_windows(mine, world * K * nw)
+    gathered = frames_to_u8(clip.flatten(0, 1)).view(world * K * nw, F, R, R, 3)
+    del clip
     sync()
     if world > 1:
         dist.barrier()
@@ -531,6 +552,9 @@ def worker(args):
                    "global_batch": world * nw * F, "resolution": R,
                    "parallelism": f"dp{world} (window sharding, RCCL all-gather of decoded frames)"},
     }
+    gib = 1024 ** 3
+    res["memory"] = {"exchange_gb": round(exchange_bytes(world, K, nw, F, R) / gib, 3),
+                     "exchange_gb_at_8_ranks_k20": round(exchange_bytes(8, 20, nw, F, R) / gib, 3)}
     if plumbing:
         want = torch.arange(world * K * nw, dtype=torch.int64) % 251
         got = gathered[:, 0, 0, 0, 0].to(torch.int64)
@@ -546,6 +570,13 @@ def worker(args):
         return
 
     window_ms = sum(a.elapsed_time(b) for a, b in ev_step) / K
+    # HBM high-water mark of the timed job (engine + this rank's frames + the exchange),
+    # before the probes below allocate their own engines
+    res["peak_hbm_gb"] = round(torch.cuda.max_memory_allocated(device) / gib, 3)
+    res["memory"].update({"engine_gb": round(engine_bytes / gib, 3), "hbm_total_gb": round(
+        torch.cuda.get_device_properties(device).total_memory / gib, 1)})
+    res["memory"]["footprint_gb_at_8_ranks_k20"] = round(res["memory"]["engine_gb"] +
+                                                         res["memory"]["exchange_gb_at_8_ranks_k20"], 3)
     probe, attn_probe, blk_probe = step_probe(eng, device)
     single = None
     if rank == 0 and nw > 1 and not args.no_single_window:

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LS_ABI_VERSION 12
+#define LS_ABI_VERSION 13
 
 typedef enum {
   LS_OK = 0,
@@ -319,6 +319,12 @@ int ls_small_linear(const float* x, int32_t M, int32_t K, const uint16_t* w, con
  * timesteps[*step] (device int32 array + device step index), out fp32 [B][dim]. */
 int ls_timestep_embed(const int32_t* timesteps, const int32_t* step, int32_t B, int32_t dim, int32_t flip,
                       float shift, float* out, void* stream);
+
+/* The same embedding for B fp32 timesteps, one per sample (ABI 13): the reference's
+ * forward accepts a python float and a per-sample timestep vector, broadcasting it over
+ * the batch (unet.py:361-376); ts device fp32 [B], out fp32 [B][dim]. */
+int ls_timestep_embed_f32(const float* ts, int32_t B, int32_t dim, int32_t flip, float shift, float* out,
+                          void* stream);
 
 /*
  * CFG combine + DDIMScheduler.step (eta = 0) fused, then re-packs the next UNet

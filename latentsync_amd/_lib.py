@@ -10,7 +10,18 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LS_HIP_LIB", os.path.join(HERE, "libls_hip.so"))
-ABI_VERSION = 12
+ABI_VERSION = 13
+
+
+
+def ab_switch(name: str, default: str) -> str:
+    """An A/B switch of the host dispatch, read from the environment ONLY in diagnostics
+    mode (LS_DIAG_BUILD=1, the same flag that builds the library's A/B kernels): the
+    default product path does not depend on the environment."""
+    if os.environ.get("LS_DIAG_BUILD", "") in ("", "0"):
+        return default
+    return os.environ.get(name, default)
+
 
 c_u16p = C.c_void_p
 c_vp = C.c_void_p
@@ -92,6 +103,7 @@ _SIGS = {
     "ls_cross_attention_block": (C.c_int, [C.POINTER(XAttnDesc), c_vp]),
     "ls_small_linear": (C.c_int, [c_vp, C.c_int32, C.c_int32, c_vp, c_vp, C.c_int32, C.c_int32, c_vp, c_vp]),
     "ls_timestep_embed": (C.c_int, [c_vp, c_vp, C.c_int32, C.c_int32, C.c_int32, C.c_float, c_vp, c_vp]),
+    "ls_timestep_embed_f32": (C.c_int, [c_vp, C.c_int32, C.c_int32, C.c_int32, C.c_float, c_vp, c_vp]),
     "ls_ddim_cfg_step": (C.c_int, [c_vp, C.c_int32, C.c_int32, C.c_int64, C.c_float, c_vp, c_vp, c_vp, c_vp,
                                    C.c_int32, c_vp]),
     "ls_prep_pixels": (C.c_int, [c_vp, C.c_int32, C.c_int32, c_vp, c_vp, c_vp, C.c_int32, c_vp]),

@@ -1204,7 +1204,7 @@ static int launch_attnw(const AttnArgs& a, int batch, int heads, hipStream_t s) 
   return check_launch("attnw_kernel");
 }
 
-static const int g_attnw_variant = getenv("LS_ATTNW_VARIANT") ? atoi(getenv("LS_ATTNW_VARIANT")) : 0;  // A/B switch
+static const int g_attnw_variant = ls_env("LS_ATTNW_VARIANT") ? atoi(ls_env("LS_ATTNW_VARIANT")) : 0;  // A/B switch
 
 static int launch_attnw512(const AttnArgs& a, int batch, int heads, hipStream_t s) {
   // same-box A/B (scripts/attn_bench.py VAE=1, 512 images at 32^2 / 64 at 64^2):
@@ -1229,7 +1229,7 @@ static int launch_attn3_(const AttnArgs& a, int batch, int heads, hipStream_t s)
   return check_launch("attn3_kernel");
 }
 
-static bool g_attn3_two = getenv("LS_ATTN3_TWO_STAGE") != nullptr;  // A/B switch: no single-tile variant
+static bool g_attn3_two = ls_env("LS_ATTN3_TWO_STAGE") != nullptr;  // A/B switch: no single-tile variant
 
 template <int KC, int ND, int DSUM>
 static int launch_attn3(const AttnArgs& a, int batch, int heads, hipStream_t s) {
@@ -1876,21 +1876,21 @@ static int launch_attn8(const AttnArgs& a, int batch, int heads, uint8_t* ws, hi
 
 using namespace ls;
 
-static bool g_attn_v1 = getenv("LS_ATTN_V1") != nullptr;  // A/B switch: force the 16-query kernel
-static bool g_attn_v3 = getenv("LS_ATTN_V3") != nullptr;  // A/B switch: attn3 for d = 40 too
+static bool g_attn_v1 = ls_env("LS_ATTN_V1") != nullptr;  // A/B switch: force the 16-query kernel
+static bool g_attn_v3 = ls_env("LS_ATTN_V3") != nullptr;  // A/B switch: attn3 for d = 40 too
 // A/B switch: d = 40 self attention on attn6 (32x32x16); measured 3 % slower than attn5 at 48
 // windows (1670 vs 1620 us per call, profiles/r04b_attn6_vs_attn5_ab.txt), so attn5 stays the default
 #ifdef LS_DIAG_KERNELS
-static bool g_attn6 = getenv("LS_ATTN6") != nullptr;
+static bool g_attn6 = ls_env("LS_ATTN6") != nullptr;
 #else
 static bool g_attn6 = false;
 #endif
 namespace ls {
 void attn_set_attn6(bool on) { g_attn6 = on; }  // ls_set_tuning key 9 (diagnostics build)
 }
-static bool g_attnw_off = getenv("LS_ATTNW_OFF") != nullptr;  // A/B switch: d = 512 on attn_kernel
-static bool g_seq_valu = getenv("LS_ATTN_SEQ_VALU") != nullptr;  // A/B switch: dot-product short-sequence kernel
-static bool g_seq160_valu = getenv("LS_ATTN_SEQ160_VALU") != nullptr;  // A/B switch: ... for d = 160 only
+static bool g_attnw_off = ls_env("LS_ATTNW_OFF") != nullptr;  // A/B switch: d = 512 on attn_kernel
+static bool g_seq_valu = ls_env("LS_ATTN_SEQ_VALU") != nullptr;  // A/B switch: dot-product short-sequence kernel
+static bool g_seq160_valu = ls_env("LS_ATTN_SEQ160_VALU") != nullptr;  // A/B switch: ... for d = 160 only
 
 static AttnArgs attn_args(const ls_attn_desc* d) {
   AttnArgs a;
@@ -1942,7 +1942,7 @@ extern "C" int ls_attention_fp8(const ls_attn_desc* d, void* workspace, size_t w
   const AttnArgs a = attn_args(d);
   hipStream_t s = (hipStream_t)stream;
   uint8_t* ws = (uint8_t*)workspace;
-  static const int variant = getenv("LS_ATTN8_VARIANT") ? atoi(getenv("LS_ATTN8_VARIANT")) : 0;  // A/B switch
+  static const int variant = ls_env("LS_ATTN8_VARIANT") ? atoi(ls_env("LS_ATTN8_VARIANT")) : 0;  // A/B switch
   if (D == 40) {
     if (variant == 1) return launch_attn8<40, 2, 2, false, 3>(a, d->batch, d->heads, ws, s);
     if (variant == 2) return launch_attn8<40, 2, 2, true, 2>(a, d->batch, d->heads, ws, s);

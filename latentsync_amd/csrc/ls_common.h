@@ -2,10 +2,23 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <atomic>
 #include <string>
 
 #include "../../include/ls_hip.h"
+
+// A/B switches read from the environment exist only in the diagnostics build
+// (LS_DIAG_KERNELS, LS_DIAG_BUILD=1): in the default library no dispatch decision and no
+// weight layout depends on the environment -- tuning goes through ls_set_tuning.
+static inline const char* ls_env(const char* name) {
+#ifdef LS_DIAG_KERNELS
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));

@@ -34,6 +34,21 @@ __global__ void timestep_embed_kernel(const int* ts, const int* step, int B, int
   }
 }
 
+// The same embedding for one fp32 timestep per sample (blockIdx.x = sample): forward()'s
+// float timesteps and distinct per-sample values, which the reference broadcasts over the
+// batch (unet.py:361-376; get_timestep_embedding casts t to fp32 before the product).
+__global__ void timestep_embed_f32_kernel(const float* ts, int dim, int flip, float shift, float* out) {
+  const int half = dim / 2;
+  const float t = ts[blockIdx.x];
+  float* o = out + (long)blockIdx.x * dim;
+  for (int i = threadIdx.x; i < half; i += blockDim.x) {
+    const float e = expf(-9.210340371976184f * (float)i / ((float)half - shift));
+    const float arg = t * e;
+    const float sn = sinf(arg), cs = cosf(arg);
+    if (flip) { o[i] = cs; o[half + i] = sn; } else { o[i] = sn; o[half + i] = cs; }
+  }
+}
+
 // y[m, n] = sum_k act(x[m, k]) * W[n, k] + b[n]; one wave per output column n,
 // rows in chunks of SL_ROWS per block (grid.y), the chunk's x cached in LDS.
 constexpr int SL_ROWS = 8;
@@ -235,6 +250,13 @@ extern "C" int ls_timestep_embed(const int32_t* ts, const int32_t* step, int32_t
   if (!ts || !step || !out || dim % 2 || B <= 0) return fail(LS_ERR_INVALID, "ls_timestep_embed: bad arguments");
   timestep_embed_kernel<<<1, 256, 0, (hipStream_t)stream>>>(ts, step, B, dim, flip, shift, out);
   return check_launch("timestep_embed_kernel");
+}
+
+extern "C" int ls_timestep_embed_f32(const float* ts, int32_t B, int32_t dim, int32_t flip, float shift, float* out,
+                                     void* stream) {
+  if (!ts || !out || dim % 2 || B <= 0) return fail(LS_ERR_INVALID, "ls_timestep_embed_f32: bad arguments");
+  timestep_embed_f32_kernel<<<B, 256, 0, (hipStream_t)stream>>>(ts, dim, flip, shift, out);
+  return check_launch("timestep_embed_f32_kernel");
 }
 
 extern "C" int ls_small_linear(const float* x, int32_t M, int32_t K, const uint16_t* w, const float* bias, int32_t N,

@@ -391,7 +391,7 @@ extern "C" int ls_feedforward(const ls_ff_desc* d, void* stream) {
   a.w2 = (const u16*)d->w2; a.b2 = d->b2; a.y = (u16*)d->y; a.M = d->M; a.ldx = d->ldx; a.ldy = d->ldy;
   constexpr int C = 320, I = 1280;
 #ifdef LS_DIAG_KERNELS
-  static const bool pair = getenv("LS_FF_PAIR") != nullptr && atoi(getenv("LS_FF_PAIR")) != 0;  // A/B switch
+  static const bool pair = ls_env("LS_FF_PAIR") != nullptr && atoi(ls_env("LS_FF_PAIR")) != 0;  // A/B switch
   if (pair) {
     const size_t shm = (size_t)2 * (64 * (C / 64) * 8 + C * 4) * 16 + 2 * I * sizeof(float) + 4 * 2 * 2 * 64 * 8;
     LS_SET_MAX_DYN_SHM((ff_pair_kernel<C, I>), (int)shm);

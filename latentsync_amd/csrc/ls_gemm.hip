@@ -2493,19 +2493,18 @@ __global__ void __launch_bounds__(TH_ / 4 * 128, 16 / TH_) conv3x3_halo_kernel(C
 }
 
 // ---------------------------------------------------------------- host side
-static bool g_force_regstage = getenv("LS_GEMM_REGSTAGE") != nullptr;
+static bool g_force_regstage = ls_env("LS_GEMM_REGSTAGE") != nullptr;
 // A/B switch: 3x3 weights packed tap-major (packing.py reads the same variable)
-static const bool g_w3_tapmajor = getenv("LS_W3_TAPMAJOR") != nullptr;
-static const int g_gemm_gm = getenv("LS_GEMM_GM") ? atoi(getenv("LS_GEMM_GM")) : 0;  // A/B switch: tile raster
-static const bool g_gm_shortk = getenv("LS_GEMM_GM_SHORTK") == nullptr || atoi(getenv("LS_GEMM_GM_SHORTK")) != 0;
+static const int g_gemm_gm = ls_env("LS_GEMM_GM") ? atoi(ls_env("LS_GEMM_GM")) : 0;  // A/B switch: tile raster
+static const bool g_gm_shortk = ls_env("LS_GEMM_GM_SHORTK") == nullptr || atoi(ls_env("LS_GEMM_GM_SHORTK")) != 0;
 static int g_force_tile = 0, g_force_split = 0, g_bk = 64;
 // ablation bits (diagnostics; tuning key 4 or LS_GEMM_ABLATE): 1 no MFMA, 2 no operand DMA,
 // 4 no output store, 8 the general epilogue arithmetic even where the short path applies
-static int g_ablate = getenv("LS_GEMM_ABLATE") ? atoi(getenv("LS_GEMM_ABLATE")) : 0;
+static int g_ablate = ls_env("LS_GEMM_ABLATE") ? atoi(ls_env("LS_GEMM_ABLATE")) : 0;
 
 struct TileCfg { int bm, bn, split; };
 // A/B switch (LS_GEMM_BIG1280=0): the N = 1280 linears back on 128 x 160 tiles
-static bool g_big1280 = getenv("LS_GEMM_BIG1280") == nullptr || atoi(getenv("LS_GEMM_BIG1280")) != 0;
+static bool g_big1280 = ls_env("LS_GEMM_BIG1280") == nullptr || atoi(ls_env("LS_GEMM_BIG1280")) != 0;
 
 // Tile + split-K choice by a small cost model.  A CU runs up to R blocks of a tile
 // at once (LDS-limited: 2 for the 4-wave 128-row tiles, 1 for the 8-wave 256x256);
@@ -2552,9 +2551,9 @@ static TileCfg pick_tile(long M, int N, int ktiles, bool allow_split, bool big_o
 }
 
 // ---- row-block GEMM dispatch (gemm_rowblock_kernel)
-static bool g_rowblock = getenv("LS_GEMM_NO_ROWBLOCK") == nullptr;
-static bool g_rowblock640 = getenv("LS_GEMM_NO_ROWBLOCK640") == nullptr;
-static bool g_rb640_res = getenv("LS_GEMM_RB640_RES") != nullptr;  // A/B switch: K = 640 residual GEMMs too
+static bool g_rowblock = ls_env("LS_GEMM_NO_ROWBLOCK") == nullptr;
+static bool g_rowblock640 = ls_env("LS_GEMM_NO_ROWBLOCK640") == nullptr;
+static bool g_rb640_res = ls_env("LS_GEMM_RB640_RES") != nullptr;  // A/B switch: K = 640 residual GEMMs too
 
 static bool rowblock_ok(const ls_conv_desc* d, const ConvArgs& a) {
   if (!g_rowblock || g_force_tile || g_force_regstage || d->ksize != 1 || a.C2) return false;
@@ -2588,7 +2587,7 @@ static void launch_rowblock2(const ConvArgs& a, int grid, hipStream_t s) {
 // K = 640 with two 16-row fragments per wave (256-row blocks, half the W-fragment LDS reads
 // per MFMA, 160 A registers): default since r04x (step 215.3 -> 212.2 ms at 48 windows, three
 // same-box alternations); tuning key 15 / LS_RB640_FM2=0: one fragment per wave
-static bool g_rb640_fm2 = getenv("LS_RB640_FM2") == nullptr || atoi(getenv("LS_RB640_FM2")) != 0;
+static bool g_rb640_fm2 = ls_env("LS_RB640_FM2") == nullptr || atoi(ls_env("LS_RB640_FM2")) != 0;
 
 static bool rb640_fm2(int flags);
 
@@ -2681,9 +2680,9 @@ static void launch_dma1(const ConvArgs& a, int grid, hipStream_t s) {
   conv_gemm_dma_kernel<BM, BN, WM, WN, KS, TAPU, NST, BK, EPI, BUF><<<grid, WM * WN * 64, shm, s>>>(a);
 }
 
-static bool g_no_buf_dma = getenv("LS_GEMM_GLDS") != nullptr;  // A/B switch: global_load_lds addressing
+static bool g_no_buf_dma = ls_env("LS_GEMM_GLDS") != nullptr;  // A/B switch: global_load_lds addressing
 #ifdef LS_DIAG_KERNELS  // measured and rejected: diagnostics build only
-static int g_rs = getenv("LS_GEMM_RS") ? atoi(getenv("LS_GEMM_RS")) : 0;  // A/B switch: register-staged buffer loads
+static int g_rs = ls_env("LS_GEMM_RS") ? atoi(ls_env("LS_GEMM_RS")) : 0;  // A/B switch: register-staged buffer loads
 
 template <int BM, int BN, int WM, int WN, int KS, int EPI>
 static void launch_rs(const ConvArgs& a, int grid, hipStream_t s) {
@@ -2691,7 +2690,7 @@ static void launch_rs(const ConvArgs& a, int grid, hipStream_t s) {
   LS_SET_MAX_DYN_SHM((conv_gemm_rs_kernel<BM, BN, WM, WN, KS, EPI>), (int)shm);
   conv_gemm_rs_kernel<BM, BN, WM, WN, KS, EPI><<<grid, WM * WN * 64, shm, s>>>(a);
 }
-static bool g_areg = getenv("LS_GEMM_AREG") ? atoi(getenv("LS_GEMM_AREG")) != 0 : false;  // A/B switch: 1x1 A in registers
+static bool g_areg = ls_env("LS_GEMM_AREG") ? atoi(ls_env("LS_GEMM_AREG")) != 0 : false;  // A/B switch: 1x1 A in registers
 
 template <int BM, int BN, int WM, int WN, int EPI>
 static void launch_areg(const ConvArgs& a, int grid, hipStream_t s) {
@@ -2701,7 +2700,7 @@ static void launch_areg(const ConvArgs& a, int grid, hipStream_t s) {
 }
 #endif  // LS_DIAG_KERNELS
 
-static bool g_no_buf_ups = getenv("LS_GEMM_UPS_GLDS") != nullptr;  // A/B switch: ... for upsampling convs only
+static bool g_no_buf_ups = ls_env("LS_GEMM_UPS_GLDS") != nullptr;  // A/B switch: ... for upsampling convs only
 
 // operand DMA through buffer descriptors: 1x1 with K == Cin, Cin % 64 == 0; tap-major 3x3,
 // stride 1 or 2, pad 0 or 1, or nearest-x2 upsample with pad 1; C1 % 64 == 0 (a K-tile never straddles the
@@ -2819,10 +2818,10 @@ static void launch_cfg(const ConvArgs& a, int ks, bool tapu, int grid, hipStream
 }
 
 // ---- halo-tile 3x3 conv dispatch (conv3x3_halo_kernel)
-static bool g_halo = getenv("LS_HALO") == nullptr || atoi(getenv("LS_HALO")) != 0;  // A/B switch: LS_HALO=0
+static bool g_halo = ls_env("LS_HALO") == nullptr || atoi(ls_env("LS_HALO")) != 0;  // A/B switch: LS_HALO=0
 // A/B switch (tuning key 13): 128-channel tiles where both divide N (3-slot weight ring
 // instead of 2 at BN 160)
-static bool g_halo_bn128 = getenv("LS_HALO_BN128") != nullptr;
+static bool g_halo_bn128 = ls_env("LS_HALO_BN128") != nullptr;
 
 // patch width of the halo conv for this call (0: not taken)
 static int halo_tw(const ls_conv_desc* d, const ConvArgs& a) {
@@ -2870,7 +2869,7 @@ static void launch_halo2(const ConvArgs& a, hipStream_t s) {
 // time: VAE 128 ch at 256^2 17.67 -> 17.23 ms, 128 -> 256 at 128^2 8.74 -> 8.43 ms, 256 at
 // 128^2 a tie; at Cin 512 (8 chunks) the 2-slot weight ring loses to the 1-block form's 3
 // slots (13.12 -> 13.55 ms at 64^2), profiles/r05k_halo_ab.txt.  A/B switch LS_HALO_TH8=0.
-static bool g_halo_th8 = getenv("LS_HALO_TH8") == nullptr || atoi(getenv("LS_HALO_TH8")) != 0;
+static bool g_halo_th8 = ls_env("LS_HALO_TH8") == nullptr || atoi(ls_env("LS_HALO_TH8")) != 0;
 
 template <int TW>
 static void launch_halo1(const ConvArgs& a, hipStream_t s) {
@@ -2888,7 +2887,7 @@ static void launch_halo(const ConvArgs& a, int tw, hipStream_t s) {
 // 256 x 128 tiles (8 waves as 4 x 2, 64 x 64 each) with a 3-stage LDS ring (147 KB) for the
 // short-K linears (K <= 1280, N % 128 == 0): two K-tiles of operand DMA in flight instead of
 // one.  (A/B switch LS_GEMM_T256=0/1; tile id 260.  256 x 160 would leave 2.5 B pieces per thread.)
-static int g_t256 = getenv("LS_GEMM_T256") ? atoi(getenv("LS_GEMM_T256")) : 0;
+static int g_t256 = ls_env("LS_GEMM_T256") ? atoi(ls_env("LS_GEMM_T256")) : 0;
 
 #endif  // LS_DIAG_KERNELS
 
@@ -2930,7 +2929,7 @@ static int build_args(const ls_conv_desc* d, ConvArgs& a, TileCfg& t, int& split
   if (a.cs_out && (M % CS_ROWS || d->N % 8 || d->ldy % 8 || d->act == LS_ACT_GEGLU || d->y_f32))
     return fail(LS_ERR_INVALID, "ls_conv2d: gn_colsum_out needs M % 128 == 0, N % 8 == 0, bf16 output, no GEGLU");
   a.ablate = g_ablate;
-  a.ccm = (d->ksize == 3 && Cin % 64 == 0 && !g_w3_tapmajor) ? 1 : 0;
+  a.ccm = (d->ksize == 3 && Cin % 64 == 0) ? 1 : 0;
   a.gm = 1;  // (set with the tile below)
   a.ktiles = d->K / 64;
   t = pick_tile(M, d->N, a.ktiles, d->split_k <= 0 && d->workspace != nullptr,

@@ -348,7 +348,7 @@ extern "C" int ls_temporal_attention(const ls_tattn_desc* d, void* stream) {
   a.eps = d->eps > 0.f ? d->eps : 1e-5f;
   a.ablate = 0;
 #ifdef LS_TATTN_ABLATE
-  if (const char* e = getenv("LS_TATTN_ABLATE")) a.ablate = atoi(e);
+  if (const char* e = ls_env("LS_TATTN_ABLATE")) a.ablate = atoi(e);
 #endif
   const int grid = d->n_samples * a.blocks_per_sample;
   hipStream_t s = (hipStream_t)stream;

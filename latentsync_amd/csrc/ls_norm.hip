@@ -402,7 +402,7 @@ extern "C" int ls_groupnorm_apply(const uint16_t* x1, const uint16_t* x2, int32_
   const int ccb = std::min(CC, 256);
   const int ppb = std::max(1, 256 / ccb);
   const int threads = (ppb * ccb + 63) / 64 * 64;  // 1280 channels: 3 waves, 160 live lanes
-  static const bool v1 = getenv("LS_GN_APPLY_V1") != nullptr;  // A/B switch: the grid-stride kernel
+  static const bool v1 = ls_env("LS_GN_APPLY_V1") != nullptr;  // A/B switch: the grid-stride kernel
   constexpr int U = 4;
   const long ublocks = (n_pix + (long)U * ppb - 1) / ((long)U * ppb);
   // (C >= 1280 -- one pixel per block pass -- stays on the grid-stride kernel: 37 vs 41 us

@@ -7,7 +7,6 @@ Activations are NHWC bf16: (images, H, W, C) with frames folded into images.
 """
 import ctypes as C
 import math
-import os
 
 import torch
 
@@ -15,7 +14,7 @@ from . import _lib
 from ._lib import check
 
 ACT_NONE, ACT_GEGLU, ACT_GELU, ACT_SILU = 0, 1, 2, 3
-_GN_EPILOGUE = os.environ.get("LS_GN_EPILOGUE", "1") != "0"  # A/B switch: 0 = GroupNorm stats by read pass
+_GN_EPILOGUE = _lib.ab_switch("LS_GN_EPILOGUE", "1") != "0"  # A/B switch (diagnostics): 0 = GN stats by read pass
 GN_SLOT_ROWS = 128  # LS_GN_SLOT_ROWS
 
 
@@ -411,6 +410,17 @@ def timestep_embed(timesteps_i32, step_i32, B, dim, flip=True, shift=0.0, out=No
         out = torch.empty((B, dim), dtype=torch.float32, device=timesteps_i32.device)
     check(lib.ls_timestep_embed(_p(timesteps_i32), _p(step_i32), B, dim, int(flip), float(shift), _p(out), _stream()),
           "ls_timestep_embed")
+    return out
+
+
+def timestep_embed_f32(t_f32, dim, flip=True, shift=0.0, out=None):
+    """One embedding row per fp32 timestep (forward()'s float / per-sample timesteps)."""
+    lib = _lib.load()
+    B = t_f32.numel()
+    if out is None:
+        out = torch.empty((B, dim), dtype=torch.float32, device=t_f32.device)
+    check(lib.ls_timestep_embed_f32(_p(t_f32), B, dim, int(flip), float(shift), _p(out), _stream()),
+          "ls_timestep_embed_f32")
     return out
 
 

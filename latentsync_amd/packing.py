@@ -8,12 +8,7 @@ the kernels consume (done at load / .to(device), never per step).
                  column 32b+i = h_{16b+i}, 32b+16+i = g_{16b+i} (epilogue pairs)
   fused q|k|v    rows concatenated (self-attention shares one LN output)
 """
-import os
-
 import torch
-
-# A/B switch shared with libls_hip.so: 3x3 weights tap-major for every Cin
-W3_TAPMAJOR = os.environ.get("LS_W3_TAPMAJOR") is not None
 
 
 def _r8(n):
@@ -40,7 +35,7 @@ def pack_weight(w: torch.Tensor, cin_pad: int = None, n_pad: int = None) -> torc
     if ip != I:
         w = torch.cat([w, torch.zeros(O, ip - I, kh, kw, dtype=w.dtype)], 1)
     w = w.permute(0, 2, 3, 1)  # (O, kh, kw, ip)
-    if kh == 3 and ip % 64 == 0 and not W3_TAPMAJOR:
+    if kh == 3 and ip % 64 == 0:
         # channel-chunk-major: k = (ci / 64) * 576 + tap * 64 + ci % 64 (the 9 taps of a
         # 64-channel chunk are consecutive K-tiles; ls_conv2d's gather follows, ls_hip.h)
         w = w.reshape(O, 9, ip // 64, 64).permute(0, 2, 1, 3).reshape(O, 9 * ip)

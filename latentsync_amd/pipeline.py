@@ -88,13 +88,24 @@ def read_video_frames(video_path):
     return fr
 
 
-def frames_to_u8(frames):
+U8_CHUNK = 256  # frames per conversion chunk of frames_to_u8 (bounds its fp32 temporaries)
+
+
+def frames_to_u8(frames, out=None):
     """(n,3,R,R) fp32 pasted frames in [-1,1] -> (n,R,R,3) uint8 with exactly the
     paste-back kernel's rounding (clamp(x/2+0.5, 0, 1)*255, truncated; fp32 throughout,
     x/2 is exact so no contraction can change it) -- the u8 of the gathered clip is
-    derived from the one fp32 all-gather instead of being gathered a second time."""
-    u = ((frames / 2 + 0.5).clamp_(0, 1) * 255).to(torch.uint8)
-    return u.permute(0, 2, 3, 1).contiguous()
+    derived from the one fp32 all-gather instead of being gathered a second time.
+    Converted in chunks of U8_CHUNK frames, so the temporaries stay 2 x U8_CHUNK fp32
+    frames whatever n is (a whole job's gathered frames reach ~100 GB per rank at
+    8 ranks, bench.py)."""
+    n, _, R, W = frames.shape
+    if out is None:
+        out = torch.empty((n, R, W, 3), dtype=torch.uint8, device=frames.device)
+    for i in range(0, n, U8_CHUNK):
+        u = ((frames[i:i + U8_CHUNK] / 2 + 0.5).clamp_(0, 1) * 255).to(torch.uint8)
+        out[i:i + U8_CHUNK].copy_(u.permute(0, 2, 3, 1))
+    return out
 
 
 # Graph lifetime.  A hipGraph must not be destroyed while a stream is capturing (the
@@ -386,8 +397,8 @@ class LipsyncPipeline:
         mask = mask.to(self.device, torch.float32)
         n_inf = math.ceil(n / num_frames)
         size = [min(num_frames, n - i * num_frames) for i in range(n_inf)]
-        # With torch.distributed initialised, rank r runs windows r, r+W, ... and the
-        # decoded frames are all-gathered once at the end (shard.py).  Every rank
+        # With torch.distributed initialised, rank r runs a contiguous block of windows
+        # and the decoded frames are all-gathered once at the end (shard.py).  Every rank
         # still draws every window's VAE noise so the result is independent of W.
         world, rank = shard.world_and_rank()
         mine = shard.rank_windows(n_inf, world, rank)

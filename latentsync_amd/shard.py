@@ -2,10 +2,12 @@
 
 Windows of a clip are independent (lipsync_pipeline.py:500-575 slices its own
 latents, faces and audio per window; DDIM with eta=0 carries no state across
-windows), so a clip shards as whole windows: rank r runs windows r, r+W, r+2W, ...
-(round-robin keeps ranks within one window of each other on ragged counts).
-The only exchange is one all-gather of the decoded frames after the loop, which
-puts every window back in clip order on every rank.
+windows), so a clip shards as whole windows.  Rank r owns the contiguous block
+[r*per, (r+1)*per) of the clip's windows, per = ceil(n / W): the busiest rank holds
+ceil(n / W) windows, as with any balanced split, and the rank-major result of the one
+all-gather is already clip order -- no reordering copy after the exchange.  The only
+exchange is that all-gather of the decoded frames after the loop, which puts every
+window back in clip order on every rank.
 """
 import math
 
@@ -19,19 +21,37 @@ def world_and_rank(group=None):
     return 1, 0
 
 
+def windows_per_rank(n_windows: int, world: int) -> int:
+    """Windows of the busiest rank (the slab size every rank contributes to the gather)."""
+    return math.ceil(n_windows / world) if n_windows > 0 else 0
+
+
 def rank_windows(n_windows: int, world: int, rank: int):
-    """Window indices owned by `rank` (round-robin)."""
+    """Window indices owned by `rank`: a contiguous block of windows_per_rank windows
+    (the last ranks hold fewer, or none, when n_windows % world != 0)."""
     if not 0 <= rank < world:
         raise ValueError(f"rank {rank} outside world {world}")
-    return list(range(rank, n_windows, world))
+    per = windows_per_rank(n_windows, world)
+    return list(range(min(n_windows, rank * per), min(n_windows, (rank + 1) * per)))
+
+
+def gather_bytes(n_windows: int, world: int, window_bytes: int) -> int:
+    """Bytes gather_windows allocates on each rank for n_windows windows of window_bytes:
+    the receive buffer (world * per windows) plus, on a rank holding fewer than per
+    windows, its zero-padded send slab.  Nothing when world == 1 (the input is returned)."""
+    if world == 1:
+        return 0
+    per = windows_per_rank(n_windows, world)
+    return (world + 1) * per * window_bytes
 
 
 def gather_windows(local: torch.Tensor, n_windows: int, group=None) -> torch.Tensor:
     """All-gather per-rank window outputs into clip order.
 
-    local: (len(rank_windows(n_windows, W, r)), *S) in the order rank_windows
-    returns.  Returns (n_windows, *S) on every rank.  One collective: the
-    per-rank slabs are padded to ceil(n_windows / W) windows so a single
+    local: (len(rank_windows(n_windows, W, r)), *S), the rank's block in order.
+    Returns (n_windows, *S) on every rank -- a view of the one receive buffer, whose
+    rank-major layout is clip order (no index_select copy).  One collective: the
+    per-rank slabs are padded to windows_per_rank windows so a single
     all_gather_into_tensor (RCCL over xGMI) moves them."""
     world, rank = world_and_rank(group)
     n_local = len(rank_windows(n_windows, world, rank))
@@ -39,7 +59,7 @@ def gather_windows(local: torch.Tensor, n_windows: int, group=None) -> torch.Ten
         raise ValueError(f"rank {rank} holds {local.shape[0]} windows, expected {n_local}")
     if world == 1:
         return local
-    per = math.ceil(n_windows / world)
+    per = windows_per_rank(n_windows, world)
     S = tuple(local.shape[1:])
     if n_local == per:
         buf = local.contiguous()
@@ -51,5 +71,4 @@ def gather_windows(local: torch.Tensor, n_windows: int, group=None) -> torch.Ten
         dist.all_gather_into_tensor(out, buf, group=group)
     else:  # gloo (CPU tests): same layout through the list form
         dist.all_gather(list(out.chunk(world)), buf, group=group)
-    order = torch.tensor([(i % world) * per + i // world for i in range(n_windows)], device=out.device)
-    return out.index_select(0, order)
+    return out[:n_windows]

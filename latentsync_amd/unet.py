@@ -22,25 +22,25 @@ activations with frames folded into the image index:
       attention over frames via strided views -> out-proj) -> GEGLU FF -> proj_out
 """
 import math
-import os
 from dataclasses import dataclass
 
 import torch
 
-from . import ops
+from . import _lib, ops
 from .config import STAGE2_MODEL
 from .packing import geglu_interleave, pack_ff_w2, pack_weight, pad_bias
 from .schema import unet_param_shapes
 from .weights import fill_state_dict
 
-# LS_FUSED_TEMPORAL=0: the motion attention as q|k|v GEMM + ls_attention (A/B switch)
-_FUSED_TEMPORAL = os.environ.get("LS_FUSED_TEMPORAL", "1") != "0"
-# LS_FUSED_FF=0: the FeedForward as GEGLU row-block GEMM + W2 GEMM (A/B switch)
-_FUSED_FF = os.environ.get("LS_FUSED_FF", "1") != "0"
+# A/B switches (read from the environment only in diagnostics mode, _lib.ab_switch):
+# LS_FUSED_TEMPORAL=0: the motion attention as q|k|v GEMM + ls_attention
+_FUSED_TEMPORAL = _lib.ab_switch("LS_FUSED_TEMPORAL", "1") != "0"
+# LS_FUSED_FF=0: the FeedForward as GEGLU row-block GEMM + W2 GEMM
+_FUSED_FF = _lib.ab_switch("LS_FUSED_FF", "1") != "0"
 # LS_FUSED_XATTN=1: the audio cross-attention branch at C = 320 as ONE ls_cross_attention_block
 # launch instead of q GEMM + ls_attention + out GEMM.  Off by default: measured 1-2 ms per
 # 48-window step SLOWER than the three launches (profiles/r04k_step_ab.txt)
-_FUSED_XATTN = os.environ.get("LS_FUSED_XATTN", "0") == "1"
+_FUSED_XATTN = _lib.ab_switch("LS_FUSED_XATTN", "0") == "1"
 
 
 def _ff(h, st, ff1, ff2, ff2p):
@@ -405,23 +405,28 @@ class _DeviceUNet:
                     yield a
         yield self.mid[1]
 
-    def temb(self, ts_i32, step_i32, B):
-        """The time embedding projected for every resnet: ONE row, because every sample of
-        the batch has the same timestep (the reference expands one t over the batch,
-        unet.py:361-374; forward() refuses distinct per-sample values) -- the resnets read it
-        as a row vector spanning all B samples.  (Computed per sample until round 5: 48
-        identical rows through three GEMVs, 0.8 ms of a 48-window step.)"""
-        t = ops.timestep_embed(ts_i32, step_i32, 1, self.boc[0], self.flip, self.shift)
+    def temb(self, ts_i32, step_i32, B, t_rows=None):
+        """The time embedding projected for every resnet.  In the denoising loop every
+        sample of the batch has the same timestep (the reference expands one t over the
+        batch, unet.py:361-374), so it is ONE row -- the resnets read it as a row vector
+        spanning all B samples (computed per sample until round 5: 48 identical rows through
+        three GEMVs, 0.8 ms of a 48-window step).  ``t_rows``: fp32 timesteps, one per
+        sample (or one for all), from forward()'s float / per-sample timestep argument."""
+        if t_rows is not None:
+            t = ops.timestep_embed_f32(t_rows, self.boc[0], self.flip, self.shift)
+        else:
+            t = ops.timestep_embed(ts_i32, step_i32, 1, self.boc[0], self.flip, self.shift)
         e1 = ops.small_linear(t, self.t1, self.t1b)
         emb = ops.small_linear(e1, self.t2, self.t2b, silu_in=True)
         return ops.small_linear(emb, self.temb_w, self.temb_b, silu_in=True)
 
     def forward(self, x_in, B, ts_i32, step_i32, audio_rows, n_audio_tok, down_res=None, mid_res=None,
-                audio_kv=None):
+                audio_kv=None, t_rows=None):
         """x_in NHWC bf16 (B*F, H, W, cin_pad) -> eps NHWC bf16 (B*F, H, W, out_channels).
-        audio_kv: the dict of audio_kv(audio_rows), precomputed once per window batch."""
+        audio_kv: the dict of audio_kv(audio_rows), precomputed once per window batch.
+        t_rows: fp32 timesteps (1 or B values) instead of ts_i32[step_i32]."""
         kvs = audio_kv or {}
-        temb = self.temb(ts_i32, step_i32, B)
+        temb = self.temb(ts_i32, step_i32, B, t_rows)
         h = ops.conv(x_in, self.conv_in, gn_out=True)
         skips = [h]
         for layers, ds in self.down:
@@ -645,20 +650,18 @@ class UNet3DConditionModel(torch.nn.Module):
             sample = 2 * sample - 1.0
         x = torch.zeros((B * F, H, W, dev.cin_pad), dtype=torch.bfloat16, device=sample.device)
         x[..., :Cin] = sample.permute(0, 2, 3, 4, 1).reshape(B * F, H, W, Cin)
+        # time (unet.py:361-376): a python int / float or a tensor of one value or one per
+        # sample, broadcast over the batch; get_timestep_embedding takes it as fp32
         if torch.is_tensor(timestep):
             tv = timestep.reshape(-1)
-            if tv.numel() == 0:
-                raise ValueError("empty timestep tensor")
-            # the reference broadcasts one timestep over the batch (unet.py:361-374); a
-            # per-sample vector would need one embedding per sample, which the
-            # inference loop never passes -- refuse it instead of using tv[0] silently
-            if tv.numel() > 1 and not bool((tv == tv[0]).all()):
-                raise NotImplementedError("per-sample timesteps (distinct values) are not on the inference path")
-            t = int(tv[0].item())
+            if tv.numel() not in (1, B):
+                raise ValueError(f"timestep has {tv.numel()} values for a batch of {B}")
         else:
-            t = int(timestep)
-        ts = torch.tensor([t], dtype=torch.int32, device=sample.device)
-        step = torch.zeros(1, dtype=torch.int32, device=sample.device)
+            tv = torch.tensor([float(timestep)], dtype=torch.float64)
+        tv = tv.to(sample.device).to(torch.float32)
+        if tv.numel() > 1 and bool((tv == tv[0]).all()):
+            tv = tv[:1]  # one row spans the batch (the denoising loop's case)
+        ts = step = None
         audio, ntok = None, 0
         if encoder_hidden_states is not None and self.add_audio_layer:
             ehs = encoder_hidden_states
@@ -682,7 +685,7 @@ class UNet3DConditionModel(torch.nn.Module):
                 r = r.unsqueeze(2)
             rb, rc, rf, rh, rw = r.shape
             mres = r.expand(B, rc, F, rh, rw).permute(0, 2, 3, 4, 1).reshape(B * F, rh, rw, rc).to(torch.bfloat16)
-        eps = dev.forward(x, B, ts, step, audio, ntok, dres, mres)
+        eps = dev.forward(x, B, ts, step, audio, ntok, dres, mres, t_rows=tv.contiguous())
         out = eps.reshape(B, F, H, W, -1)[..., :self.config.out_channels].permute(0, 4, 1, 2, 3)
         out = out.to(sample.dtype if sample.dtype.is_floating_point else torch.float32).contiguous()
         if not return_dict:

@@ -183,7 +183,8 @@ def upsample_nearest(x5):
 
 def unet_forward(sd, cfg, sample, timestep, audio):
     """UNet3DConditionModel.forward (unet.py:312-471) for the configs/unet/*.yaml
-    topology (unet.py:42-241).  sample (B,Cin,F,H,W) fp32, timestep int, audio
+    topology (unet.py:42-241).  sample (B,Cin,F,H,W) fp32, timestep an int, a float or
+    a tensor of 1 or B values (broadcast over the batch, unet.py:361-376), audio
     (B*F, 50, 384) or None.  Returns (B, Cout, F, H, W)."""
     boc = list(cfg["block_out_channels"])
     nb = len(boc)
@@ -197,7 +198,12 @@ def unet_forward(sd, cfg, sample, timestep, audio):
     if audio is not None and not cfg.get("add_audio_layer", False):
         audio = None
 
-    t = torch.full((B,), int(timestep), dtype=torch.int64)
+    if torch.is_tensor(timestep):
+        t = timestep.reshape(-1).expand(B) if timestep.numel() == 1 else timestep.reshape(-1)
+    elif isinstance(timestep, float):
+        t = torch.tensor([timestep], dtype=torch.float64).expand(B)
+    else:
+        t = torch.full((B,), int(timestep), dtype=torch.int64)
     temb = timestep_embedding(t, boc[0], cfg.get("flip_sin_to_cos", True), cfg.get("freq_shift", 0))
     emb = _lin(F.silu(_lin(temb, sd, "time_embedding.linear_1")), sd, "time_embedding.linear_2")
 

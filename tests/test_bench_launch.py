@@ -1,6 +1,6 @@
 """bench.py's multi-GPU launch path on CPU (gloo): `--gpus N` spawns N fresh worker
 processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set per worker), each rank
-owns windows r, r+N, ... and the decoded frames are all-gathered once at the end
+owns a contiguous block of the job's windows and the decoded frames are all-gathered once at the end
 (latentsync_amd/shard.py).  `--plumbing` replaces only the window compute with a
 stand-in that writes each window's global index into its frames, so the gathered
 clip order is checked exactly.  Also: a failing rank ends the job with a non-zero
@@ -27,7 +27,7 @@ def _line(r):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("n", [1, 2, 3])
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
 def test_spawned_ranks_gather_in_clip_order(n):
     r = _bench("--gpus", str(n), "--steps", "3", "--warmup", "1")
     assert r.returncode == 0, r.stderr

@@ -48,3 +48,41 @@ def test_unet_tiny_matches_reference(gpu):
 
 def test_unet_full_matches_reference(gpu):
     _run(STAGE2_MODEL, "unet_full.npz")
+
+
+@pytest.mark.parametrize("kind", ["float", "per_sample", "int_tensor"])
+def test_unet_timestep_forms(gpu, kind):
+    """forward() takes the timestep forms the reference takes (unet.py:361-376): a
+    python float (not truncated), a tensor of distinct per-sample values and a 0-d
+    integer tensor -- checked against the fp32 oracle given the same timesteps."""
+    from oracle import ref_cpu as O
+    cfg = TINY_MODEL
+    unet = UNet3DConditionModel(**cfg).init_weights(11).to("cuda").eval()
+    B, Fr, H = 2, 4, 16
+    sample = torch.randn((B, cfg["in_channels"], Fr, H, H), generator=torch.Generator().manual_seed(5))
+    audio = torch.randn((B * Fr, 50, cfg["cross_attention_dim"]), generator=torch.Generator().manual_seed(6))
+    t = {"float": 500.75, "per_sample": torch.tensor([981, 21]), "int_tensor": torch.tensor(401)}[kind]
+    with torch.no_grad():
+        out = unet(sample.cuda(), t, encoder_hidden_states=audio.cuda()).sample.float().cpu()
+        ref = O.unet_forward(unet._sd, dict(unet.config), sample, t, audio)
+    e = rel_err(out, ref)
+    print(kind, "rel_err", e)
+    assert e < TOL, e
+    if kind == "per_sample":  # sample 1 follows its own timestep, not sample 0's
+        with torch.no_grad():
+            ref0 = O.unet_forward(unet._sd, dict(unet.config), sample, 981, audio)
+        assert rel_err(out[:1], ref0[:1]) < TOL
+        assert rel_err(out[1:], ref0[1:]) > 3 * rel_err(out[1:], ref[1:])
+
+
+def test_timestep_embed_f32(gpu):
+    """ls_timestep_embed_f32 against diffusers' get_timestep_embedding (oracle) for
+    fractional and per-sample timesteps: the fraction is kept, not truncated."""
+    from latentsync_amd import ops
+    from oracle import ref_cpu as O
+    t = torch.tensor([500.75, 0.0, 999.0, 21.25])
+    got = ops.timestep_embed_f32(t.cuda(), 320, True, 0.0).cpu()
+    ref = O.timestep_embedding(t, 320, True, 0)
+    assert (got - ref).abs().max() < 2e-3, (got - ref).abs().max()
+    trunc = O.timestep_embedding(t.floor(), 320, True, 0)
+    assert (trunc - ref).abs().max() > 0.1

@@ -24,8 +24,6 @@ def test_pack3x3_order(I, kind):
     O = 3
     w = torch.arange(O * I * 9, dtype=torch.float32).reshape(O, I, 3, 3)
     p = packing.pack_weight(w)
-    if packing.W3_TAPMAJOR:
-        kind = "tap"
     for k, (tap, ci) in enumerate(_unpack_index(O, I, kind)):
         kh, kw = divmod(tap, 3)
         assert torch.equal(p[:, k], w[:, ci, kh, kw]), (k, tap, ci)
