@@ -36,13 +36,15 @@ def rank_windows(n_windows: int, world: int, rank: int):
 
 
 def gather_bytes(n_windows: int, world: int, window_bytes: int) -> int:
-    """Bytes gather_windows allocates on each rank for n_windows windows of window_bytes:
-    the receive buffer (world * per windows) plus, on a rank holding fewer than per
-    windows, its zero-padded send slab.  Nothing when world == 1 (the input is returned)."""
+    """Bytes gather_windows allocates on the busiest rank for n_windows windows of
+    window_bytes: the receive buffer (world * per windows) plus, when some rank holds
+    fewer than per windows, that rank's zero-padded send slab.  Nothing when world == 1
+    (the input is returned)."""
     if world == 1:
         return 0
     per = windows_per_rank(n_windows, world)
-    return (world + 1) * per * window_bytes
+    pad = per if n_windows < world * per else 0
+    return (world * per + pad) * window_bytes
 
 
 def gather_windows(local: torch.Tensor, n_windows: int, group=None) -> torch.Tensor:
