@@ -291,22 +291,31 @@ class WindowEngine:
 
 # Engine sizes (windows per UNet call) a clip's full windows are rounded up to, so clips of
 # different lengths share captured engines (a new size costs a warm-up run + three graph
-# captures, WindowEngine.capture_s); padding windows run and are discarded.
-WINDOW_BUCKETS = (1, 2, 4, 8, 16, 24, 32, 40, 48)
+# captures, WindowEngine.capture_s ~0.5 s); padding windows run and are discarded.  Steps of
+# 4 windows above 8, and a bucket is used only while its padding stays within MAX_PAD of
+# the clip's windows -- otherwise the engine is sized exactly (a 9-window clip runs 9, not
+# 12 or 16; 49 windows run as 2 x 28 = 56, +14 %, not 2 x 32).
+WINDOW_BUCKETS = (1, 2, 4, 6, 8, 12, 16, 20, 24, 28, 32, 36, 40, 44, 48)
+MAX_PAD = 0.2
 
 
 def plan_window_batches(full, windows_per_batch):
     """Split the full windows `full` (indices) into batches for one engine size E:
-    E = the smallest bucket (WINDOW_BUCKETS below `windows_per_batch`, plus
-    `windows_per_batch` itself) that holds ceil(len / ceil(len / windows_per_batch))
+    k = ceil(len / windows_per_batch) batches of per = ceil(len / k) windows; E = the
+    smallest bucket (WINDOW_BUCKETS below `windows_per_batch`, plus `windows_per_batch`
+    itself) >= per, or E = per when that bucket would pad more than MAX_PAD of the
     windows; batches of E consecutive windows, the last one short (the caller pads it).
     Returns (E, batches); (0, []) for no full window."""
     if not full:
         return 0, []
+    n = len(full)
     cap = max(1, int(windows_per_batch))
-    per = math.ceil(len(full) / math.ceil(len(full) / cap))
+    k = math.ceil(n / cap)
+    per = math.ceil(n / k)
     E = min(b for b in sorted({b for b in WINDOW_BUCKETS if b < cap} | {cap}) if b >= per)
-    return E, [list(full[b:b + E]) for b in range(0, len(full), E)]
+    if E * math.ceil(n / E) - n > MAX_PAD * n:
+        E = per
+    return E, [list(full[b:b + E]) for b in range(0, n, E)]
 
 
 class LipsyncPipeline:

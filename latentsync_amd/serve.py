@@ -169,9 +169,11 @@ class ProcessWorker:
     `request_timeout` seconds, or whose worker dies under it, fails with WorkerDied
     and the worker is replaced by a freshly SPAWNED child (never a re-exec of a
     process that touched the GPU), so the next request routed here is served.  The
-    failed request is answered at once; the replacement loads in the background and
-    the next request waits for its 'ready' (a replacement that fails to start fails
-    that request with WorkerDied too, and is retried on the one after)."""
+    failed request is answered at once and the replacement loads in the background:
+    the Dispatcher waits for its 'ready' (`ensure_ready`) BEFORE this worker takes
+    another request from the queue, so meanwhile the other GPUs' workers serve the
+    queue.  A replacement that fails to start fails the next request this worker takes
+    with WorkerDied ("did not start"), and another replacement is launched."""
 
     def __init__(self, rank, factory, request_timeout=1800.0, start_timeout=900.0, **job_kw):
         self.rank, self.factory, self.job_kw = rank, factory, job_kw
@@ -219,15 +221,28 @@ class ProcessWorker:
         self.launch()
         self._unready = True
 
+    def ensure_ready(self):
+        """Block until a replacement child launched after a failure reports 'ready'.
+        Returns None when the worker can take a request, else the start failure (a new
+        replacement has then been launched)."""
+        if not self._unready:
+            return None
+        try:
+            self.wait_ready()
+            self._unready = False
+            return None
+        except RuntimeError as e:
+            self._replace()
+            return str(e)
+
+    def start_failed(self, payload, err):
+        return "dead", (f"GPU worker {self.rank}: the replacement child did not start ({err}); "
+                        f"request {payload.get('id')!r} not served, another replacement launched")
+
     def _call(self, payload):
-        if self._unready:  # the replacement launched after the previous failure
-            try:
-                self.wait_ready()
-                self._unready = False
-            except RuntimeError as e:
-                self._replace()
-                return "dead", (f"GPU worker {self.rank}: the replacement child did not start ({e}); "
-                                f"request {payload.get('id')!r} not served, another replacement launched")
+        err = self.ensure_ready()  # direct callers; the Dispatcher waits before dequeuing
+        if err is not None:
+            return self.start_failed(payload, err)
         try:
             self.conn.send(payload)
             if not self.conn.poll(self.request_timeout):
@@ -290,9 +305,17 @@ class Dispatcher:
             self.tasks.append(asyncio.create_task(self._consume(w)))
 
     async def _consume(self, worker):
+        loop = asyncio.get_running_loop()
         while True:
+            start_err = None
+            if hasattr(worker, "ensure_ready"):
+                # a replacement child loads (up to start_timeout) BEFORE this consumer takes
+                # a request, so the queue drains to the ready workers meanwhile
+                start_err = await loop.run_in_executor(None, worker.ensure_ready)
             payload, fut = await self.queue.get()
             try:
+                if start_err is not None:
+                    raise WorkerDied(worker.start_failed(payload, start_err)[1])
                 res = await worker.run(payload)
                 self.served[worker.rank] += 1
                 if not fut.done():

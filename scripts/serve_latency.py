@@ -2,7 +2,10 @@
 ProcessWorker -> spawned pipeline process on cuda:0) with the stage2 UNet + full SD VAE +
 Whisper-tiny at 256^2 (random weights, synthetic clips): a 10-window clip cold (the first
 request: engine build + graph capture), the same clip warm, then an 11-window clip, which
-shares the 10-window clip's 16-window engine (pipeline.plan_window_batches).
+shares the 10-window clip's 12-window engine (pipeline.plan_window_batches), then the
+lengths the bucket padding is worst for: 9 windows (an exact 9-window
+engine, cold), 25 windows (one 28-window engine: cold, then warm) and 49 windows (2 x 28
+on the same engine).
 usage: python scripts/serve_latency.py"""
 import os
 import sys
@@ -54,12 +57,16 @@ def main():
     d = tempfile.mkdtemp(prefix="ls_serve_")
     _clip(d, "c10", 160, 6.4)
     _clip(d, "c11", 176, 7.04)
+    for w in (9, 25, 49):
+        _clip(d, f"c{w}", 16 * w, 16 * w / 25)
     worker = S.ProcessWorker(0, "serve_latency:random_stage2_pipeline", request_timeout=900.0, data_dir=d,
                              results_dir=os.path.join(d, "res"), resolution=256)
     app = S.create_app([worker])
     with TestClient(app) as c:
         for rid, vid, what in (("r1", "c10", "cold (engine build + capture)"),
-                               ("r2", "c10", "warm"), ("r3", "c11", "a longer clip, same engine bucket")):
+                               ("r2", "c10", "warm"), ("r3", "c11", "a longer clip, same engine bucket"),
+                               ("r4", "c9", "exact-size engine, cold"), ("r5", "c25", "28-window engine, cold"),
+                               ("r6", "c25", "warm"), ("r7", "c49", "2 x 28 windows, same engine")):
             t0 = time.time()
             r = c.post("/process", json={"id": rid, "video_id": vid, "audio_url": "file://" + os.path.join(d, f"{vid}.wav")})
             wall = time.time() - t0

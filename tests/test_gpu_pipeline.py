@@ -193,7 +193,7 @@ def test_engines_dropped_during_capture(gpu):
 
 
 def test_clip_lengths_share_one_engine(gpu, monkeypatch):
-    """Clips of 10 and 11 windows run through ONE captured engine (16 windows: the bucket,
+    """Clips of 10 and 11 windows run through ONE captured engine (12 windows: the bucket,
     pipeline.plan_window_batches; padding windows computed and discarded).  The windows the
     two clips have in common come out bit-identical (same engine, same per-window inputs:
     the padding windows never mix into a real one), and window 0 matches the oracle."""
@@ -219,9 +219,9 @@ def test_clip_lengths_share_one_engine(gpu, monkeypatch):
                                           all_latents=init[:, :, :n].cuda(),
                                           vae_noise=lambda i: (noise[i][0].cuda(), noise[i][1].cuda()))
         assert outs[n_win].shape == (n, 3, Rr, Rr)
-    assert list(k[-1] for k in pipe._engines) == [16], list(pipe._engines)
+    assert list(k[-1] for k in pipe._engines) == [12], list(pipe._engines)
     eng = next(iter(pipe._engines.values()))
-    print(f"engine of 16 windows: warm-up + capture {eng.capture_s:.3f} s")
+    print(f"engine of 12 windows: warm-up + capture {eng.capture_s:.3f} s")
     assert torch.equal(outs[10], outs[11][:10 * Fr])
     ref = R.pipeline_window(unet.state_dict(), dict(unet.config), vae._sd, faces[:Fr], mask, audio[:Fr],
                             init[:, :, :1], noise[0][0], noise[0][1], num_steps=steps, guidance_scale=1.0)

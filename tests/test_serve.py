@@ -264,3 +264,78 @@ def test_brightness_factor_without_darken_is_served(tmp_path):
     real = LipsyncPipeline.__new__(LipsyncPipeline)
     with pytest.raises(FileNotFoundError):
         real(**dict(kw, data_path=str(tmp_path / "absent.pth")))
+
+
+def _marker(name):
+    return os.path.join(os.environ["LS_TEST_SERVE_DIR"], name)
+
+
+def _slow_reload_factory(rank):
+    """Dies on 'die' (as _DyingPipeline); a replacement child (after the first start of
+    this rank) takes 4 s to load."""
+    m = _marker(f"started{rank}")
+    if os.path.exists(m):
+        time.sleep(4.0)
+    open(m, "w").close()
+    return _DyingPipeline()
+
+
+def test_dispatch_routes_around_a_reloading_worker(tmp_path, monkeypatch):
+    """A worker whose child died is not handed the next request while its replacement
+    loads: the consumer waits for 'ready' before dequeuing, so the other GPU's worker
+    serves the queue at once."""
+    monkeypatch.setenv("LS_TEST_SERVE_DIR", str(tmp_path))
+    for rid in ("die", "a", "b"):
+        _files(tmp_path, rid=rid)
+    kw = dict(data_dir=str(tmp_path), results_dir=str(tmp_path / "res"))
+    workers = [S.ProcessWorker(r, "test_serve:_slow_reload_factory", request_timeout=30.0, start_timeout=60.0, **kw)
+               for r in range(2)]
+
+    async def go():
+        d = S.Dispatcher(workers, queue_size=10)
+        await d.start()
+        try:
+            with pytest.raises(S.WorkerDied, match="died"):
+                await d.submit({"id": "die", "video_id": "v1", "audio_url": "x"})
+            t0 = time.time()
+            ra = await d.submit({"id": "a", "video_id": "v1", "audio_url": "x"})
+            rb = await d.submit({"id": "b", "video_id": "v1", "audio_url": "x"})
+            return time.time() - t0, ra, rb
+        finally:
+            await d.stop()
+    dt, ra, rb = asyncio.run(go())
+    assert ra["output_url"].endswith("a.npz") and rb["output_url"].endswith("b.npz")
+    assert sum(w.restarts for w in workers) == 1
+    assert dt < 3.0, dt  # served by the healthy worker, not after the 4 s reload
+
+
+def _broken_replacement_factory(rank):
+    """The first child starts; a replacement fails to start while the 'broken' marker
+    exists (exit 5) and starts normally once it is gone."""
+    m = _marker("first")
+    if os.path.exists(m) and os.path.exists(_marker("broken")):
+        raise SystemExit(5)
+    open(m, "w").close()
+    return _DyingPipeline()
+
+
+def test_process_worker_replacement_that_fails_to_start(tmp_path, monkeypatch):
+    monkeypatch.setenv("LS_TEST_SERVE_DIR", str(tmp_path))
+    for rid in ("die", "x1", "x2"):
+        _files(tmp_path, rid=rid)
+    open(_marker("broken"), "w").close()
+    w = S.ProcessWorker(0, "test_serve:_broken_replacement_factory", request_timeout=30.0, start_timeout=60.0,
+                        data_dir=str(tmp_path), results_dir=str(tmp_path / "res"))
+    w.start()
+    try:
+        with pytest.raises(S.WorkerDied, match="died"):
+            asyncio.run(w.run({"id": "die", "video_id": "v1", "audio_url": "x"}))
+        assert w.restarts == 1
+        with pytest.raises(S.WorkerDied, match="did not start"):
+            asyncio.run(w.run({"id": "x1", "video_id": "v1", "audio_url": "x"}))
+        assert w.restarts == 2
+        os.remove(_marker("broken"))  # the factory recovers: the replacement launched above starts
+        assert asyncio.run(w.run({"id": "x2", "video_id": "v1", "audio_url": "x"}))["output_url"].endswith("x2.npz")
+        assert w.restarts == 2
+    finally:
+        w.stop()
