@@ -30,6 +30,9 @@ def _bf(t):
     (4, 16, 16, 640, 0, 640, 2, False, False, True),     # no affine, residual
     (2, 32, 32, 512, 0, 512, 1, True, False, False),     # VAE 512 ch (BN 128, 8 chunks)
     (3, 48, 16, 64, 0, 256, 3, True, False, False),      # one 64-channel chunk, non-square
+    # 128-column tiles (16 x 8 form at th8 = 1) with the per-frame row vector AND the residual
+    # over a 4-frame GN sample (the TH = 8 epilogue row mapping with both)
+    (4, 32, 32, 128, 0, 256, 4, True, True, True),
 ])
 @pytest.mark.parametrize("th8", [1, 0])
 def test_halo_conv(gpu, n, H, W, C1, C2, N, ipp, aff, rowvec, res, th8):

@@ -654,3 +654,38 @@ def test_feedforward_fused(gpu, M):
     y2 = _ff(xd, st, ff1, ff2, None).float().cpu()
     assert rel_err(y - x, ref - x) < 2e-2
     assert rel_err(y, y2) < 1e-2
+
+
+@pytest.mark.parametrize("fm2", [1, 0])
+def test_rowblock640_affine_odd_sample_rows(gpu, fm2):
+    """K = 640 1x1 conv with the GroupNorm affine folded into the row-block A rows, where a
+    sample spans 384 rows (128 x odd): a 256-row block (the two-fragment K = 640 form,
+    tuning key 15) would straddle two samples and apply one sample's affine to both, so
+    that form must not take RB_AFF -- checked against fp32 per sample and
+    against the tiled path with the affine materialised."""
+    from latentsync_amd import _lib
+    lib = _lib.load()
+    n, H, W, C, N = 16, 16, 24, 640, 640   # 384 pixels per sample (imgs_per_sample 1)
+    x = bf(rnd(n, H, W, C, seed=120) * 2 + 0.5)
+    w = rnd(N, C, seed=121, scale=1 / math.sqrt(C))
+    b = rnd(N, seed=122, scale=0.1)
+    scale = 1 + 0.3 * rnd(n, C, seed=123)
+    shift = 0.5 * rnd(n, C, seed=124)
+    pk = packed(w, b, 1)
+    xd = x.to(torch.bfloat16).to(DEV)
+    aff = (scale.to(DEV), shift.to(DEV), 1, False)
+    assert lib.ls_set_tuning(15, fm2) == 0
+    try:
+        y = ops.conv(xd, pk, aff=aff, aff_materialize=True).float().cpu()
+        lib.ls_set_tuning(6, 0)
+        try:
+            y_tiled = ops.conv(xd, pk, aff=aff, aff_materialize=True).float().cpu()
+        finally:
+            lib.ls_set_tuning(6, 1)
+    finally:
+        lib.ls_set_tuning(15, 1)
+    ref = bf(x * scale[:, None, None, :] + shift[:, None, None, :]) @ w.T + b
+    per_sample = [rel_err(y[i], ref[i]) for i in range(n)]
+    print("row-block K=640 affine, per-sample rel_err max", max(per_sample))
+    assert max(per_sample) < 1e-2
+    assert rel_err(y, y_tiled) < 1e-2
