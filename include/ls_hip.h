@@ -276,6 +276,44 @@ typedef struct {
 int ls_feedforward(const ls_ff_desc* d, void* stream);
 
 /*
+ * The 32x32-level tail of a Transformer3DModel block / motion module in ONE launch (ABI
+ * 13): the attention branch's out-projection + residual, the LayerNorm, the GEGLU
+ * FeedForward + residual and proj_out + the block input, with the GroupNorm column sums
+ * of the result (replaces attention.py:174-199 attn2.to_out + norm3 + ff and :110-118
+ * proj_out; motion_module.py:262-313 the last to_out + ff_norm + ff and :126-151 proj_out):
+ *   h2 = o Wo^T + bo + h1,  y = h2 + W2 (h * gelu_erf(g)) + b2 with [h | g] = W1 LN(h2) + b1,
+ *   z  = y Wp^T + bp + xb
+ * Rows: o, h1, xb, z bf16 [M][ld*] (M % 128 == 0).  LN statistics are computed in the
+ * kernel over the bf16-rounded h2 (biased variance, eps).  Weights (packing.pack_ff_chain):
+ * wo, wp bf16 [C/32][C][32] k-step images (wp and w1 with each 32-wide k block permuted to
+ * the register order of pack_ff_w2, wo in natural order; 16-B pieces swizzled as w2); w1
+ * bf16 [2*inner][C] (GEGLU rows interleaved, LN gamma folded), b1 = b1 + W1 beta; w2 as
+ * ls_feedforward; bo, b2, bp fp32 [C].  cs_out: NULL or fp32 [M/128][2][C] column sums
+ * (Σz, Σz²) of the stored z per 128-row slot (ls_conv_desc.gn_colsum_out's layout).
+ * C = 320, inner = 1280 only.  h2 and y never reach memory.
+ */
+typedef struct {
+  const void* o;
+  const void* wo;
+  const float* bo;
+  const void* h1;
+  const void* w1;
+  const float* b1;
+  const void* w2;
+  const float* b2;
+  const void* wp;
+  const float* bp;
+  const void* xb;
+  void* z;
+  float* cs_out;
+  int64_t M;
+  int32_t ldo, ldh, ldxb, ldz, C, inner;
+  float eps;
+} ls_ff_chain_desc;
+
+int ls_ff_chain(const ls_ff_chain_desc* d, void* stream);
+
+/*
  * The audio cross-attention branch of a BasicTransformerBlock, one launch (ABI 12;
  * attention.py:174-199 norm2 + attn2, Attention.forward :250-280 with the Whisper chunks
  * as encoder_hidden_states; replaces the LN-folded to_q GEMM + ls_attention + the

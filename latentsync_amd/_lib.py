@@ -71,6 +71,13 @@ class FFDesc(C.Structure):
                 ("inner", C.c_int32)]
 
 
+class FFChainDesc(C.Structure):
+    _fields_ = [("o", c_vp), ("wo", c_vp), ("bo", c_vp), ("h1", c_vp), ("w1", c_vp), ("b1", c_vp), ("w2", c_vp),
+                ("b2", c_vp), ("wp", c_vp), ("bp", c_vp), ("xb", c_vp), ("z", c_vp), ("cs_out", c_vp),
+                ("M", C.c_int64), ("ldo", C.c_int32), ("ldh", C.c_int32), ("ldxb", C.c_int32), ("ldz", C.c_int32),
+                ("C", C.c_int32), ("inner", C.c_int32), ("eps", C.c_float)]
+
+
 class XAttnDesc(C.Structure):
     _fields_ = [("x", c_vp), ("ln_rowstats", c_vp), ("wq", c_vp), ("bq", c_vp), ("kv", c_vp), ("wo", c_vp),
                 ("bo", c_vp), ("y", c_vp), ("stats_out", c_vp), ("M", C.c_int64), ("ldx", C.c_int32),
@@ -101,6 +108,7 @@ _SIGS = {
     "ls_temporal_attention": (C.c_int, [C.POINTER(TAttnDesc), c_vp]),
     "ls_feedforward": (C.c_int, [C.POINTER(FFDesc), c_vp]),
     "ls_cross_attention_block": (C.c_int, [C.POINTER(XAttnDesc), c_vp]),
+    "ls_ff_chain": (C.c_int, [C.POINTER(FFChainDesc), c_vp]),
     "ls_small_linear": (C.c_int, [c_vp, C.c_int32, C.c_int32, c_vp, c_vp, C.c_int32, C.c_int32, c_vp, c_vp]),
     "ls_timestep_embed": (C.c_int, [c_vp, c_vp, C.c_int32, C.c_int32, C.c_int32, C.c_float, c_vp, c_vp]),
     "ls_timestep_embed_f32": (C.c_int, [c_vp, C.c_int32, C.c_int32, C.c_int32, C.c_float, c_vp, c_vp]),

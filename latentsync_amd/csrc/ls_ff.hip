@@ -66,7 +66,7 @@ __global__ void __launch_bounds__(512, 1) ff_fused_kernel(FFArgs a) {
 
   for (int i = tid; i < 2 * I / 4; i += 512) ((float4*)b1s)[i] = ((const float4*)a.b1)[i];
 
-  auto issue = [&](int c, int st) {
+  auto issue = [&](int c, int st) __attribute__((always_inline)) {
     uint4* dst = lds + st * STAGE;
 #pragma unroll
     for (int p = 0; p < PW1; ++p) {  // piece q: image p (k 64p .. 64p + 63), row (q / 8) % 64, physical chunk q % 8
@@ -178,6 +178,323 @@ __global__ void __launch_bounds__(512, 1) ff_fused_kernel(FFArgs a) {
       const float o2 = out[t][2] + b.z + __uint_as_float(rs.y << 16);
       const float o3 = out[t][3] + b.w + __uint_as_float(rs.y & 0xffff0000u);
       *(uint2*)(yr + col) = make_uint2(pack2(o0, o1), pack2(o2, o3));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// ff_chain_kernel (round 6, ABI 14 ls_ff_chain): the 32x32-level tail of a Transformer3D /
+// motion block in ONE launch -- the attention branch's out-projection + residual, the
+// LayerNorm, the GEGLU FeedForward + residual, proj_out + the block input, and the
+// GroupNorm column sums of the result for the next GroupNorm:
+//
+//   h2 = o Wo^T + bo + h1                     attn2 (attn1 without audio) to_out + residual
+//                                             (attention.py:174-199); the motion block's last
+//                                             attention to_out (motion_module.py:262-313)
+//   y  = h2 + W2 GEGLU(W1 LN(h2) + b1) + b2   norm3 + ff / ff_norm + ff, as ff_fused_kernel
+//   z  = y Wp^T + bp + xb                     proj_out + the block input (attention.py:110-118,
+//                                             motion_module.py:126-151)
+//
+// Unfused, h2 and y each make a round trip through HBM (write + read: 2 GB per call at 48
+// windows) and the two K = C projections run as separate latency-bound row-block GEMMs
+// (390 us each at 48 windows, profiles/r05f2_step_calls.txt).  Here they are two more
+// GEMM phases of the FeedForward kernel on the registers it already holds:
+//   * phase A (GEMM0): the wave's 16 o rows are the B operand (40 VGPRs, natural k order),
+//     the 20 accumulator tiles of all C outputs (80 VGPRs) start at bo; Wo streams through
+//     the LDS stages in k-step images [C rows][32 k] (a 60-KB stage holds three);
+//   * + h1, rounded to bf16 (the values the unfused path stores), the row's LayerNorm
+//     statistics (two-pass, fp32, across the 4 lane groups of a row by cross-row swaps) and
+//     LN(h2) into the GEMM1 operand registers -- in ACCUMULATOR order: k-slot (lg, e) of
+//     k-step s is column 32 s + (e < 4 ? 4 lg + e : 16 + 4 lg + e - 4), so the host packs
+//     W1's columns with that permutation (pack_ff_w2's order); the FeedForward's
+//     accumulators start at h2 + b2 (the residual);
+//   * phase B: the FeedForward chunk loop of ff_fused_kernel;
+//   * y rounded to bf16 into the operand registers (accumulator order again: Wp packed
+//     permuted), the accumulators restart at bp, phase C (GEMM3) streams Wp like Wo;
+//   * + xb, bf16; the block's 128 x C result goes through LDS once: coalesced 16-B row
+//     stores, and the GroupNorm column sums of the stored values for the block's 128-row
+//     slot (ls_conv_desc.gn_colsum_out's layout) -- so the consumer's ls_groupnorm_colsum
+//     needs no read pass.
+// Per row it reads o, h1, xb and writes z; the GEMM work grows by 2 x 2 C^2 flop per row
+// (+17 % over the FeedForward's 2 x 3 x 2 C I).
+struct FFChainArgs {
+  const u16* o;       // [M][ldo]  attention output (GEMM0's operand)
+  const u16* wo;      // [C/32][C][32]  Wo k-step images (natural k order, pieces swizzled)
+  const float* bo;    // [C]
+  const u16* h1;      // [M][ldh]  GEMM0's residual
+  const u16* w1;      // [2I][C]   GEGLU W1: rows interleaved (h, g), LN gamma folded, k permuted
+  const float* b1;    // [2I]
+  const u16* w2;      // [I/32][C][32] (pack_ff_w2)
+  const float* b2;    // [C]
+  const u16* wp;      // [C/32][C][32]  Wp k-step images (k permuted, pieces swizzled)
+  const float* bp;    // [C]
+  const u16* xb;      // [M][ldxb] proj_out's residual (the block input)
+  u16* z;             // [M][ldz]
+  float* cs_out;      // [M/128][2][C] GroupNorm column sums of z, or null
+  long M;
+  int ldo, ldh, ldxb, ldz;
+  float eps;          // the LayerNorm's eps
+};
+
+template <int C, int I>
+__global__ void __launch_bounds__(512, 1) ff_chain_kernel(FFChainArgs a) {
+  constexpr int KT = C / 32;              // k-steps of every C-wide contraction
+  constexpr int NCH = I / 32;             // FeedForward inner chunks
+  constexpr int WIMG = 64 * (C / 64) * 8; // uint4: W1 chunk
+  constexpr int W2IMG = C * 4;            // uint4: one [C][32] k-step image (W2 chunk, Wo / Wp k-step)
+  constexpr int STAGE = WIMG + W2IMG;
+  constexpr int KPS = STAGE / W2IMG;      // k-step images per stage in phases A / C
+  constexpr int NA = (KT + KPS - 1) / KPS;  // stages of phase A (and of phase C)
+  constexpr int NT2 = C / 16;             // output tiles
+  constexpr int PW1 = WIMG / 512;
+  constexpr int UW2 = W2IMG / 64;
+  constexpr int PD1 = 2, PD2 = 6;
+  constexpr int ZP = C + 8;               // LDS pitch (bf16) of the block's result image
+  static_assert(STAGE % W2IMG == 0 && KPS >= 1 && 2 * STAGE * 16 >= 128 * ZP * 2 + 4 * 80 * 8 * 4, "ff_chain LDS");
+  static_assert(C == 320 && I == 1280, "ff_chain shape");
+  extern __shared__ __attribute__((aligned(16))) uint4 lds[];  // [2][STAGE], then b1 (2I fp32)
+  float* b1s = (float*)(lds + 2 * STAGE);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l16 = lane & 15, lg = lane >> 4;
+  const long row0 = (long)blockIdx.x * 128;
+  const long row = row0 + wid * 16 + l16;  // host: M % 128 == 0
+
+  for (int i = tid; i < 2 * I / 4; i += 512) ((float4*)b1s)[i] = ((const float4*)a.b1)[i];
+
+  // chunk g of the launch: [0, NA) Wo stages, [NA, NA + NCH) FeedForward chunks, then Wp stages
+  auto issue = [&](int g, int st) {
+    uint4* dst = lds + st * STAGE;
+    if (g < NA || g >= NA + NCH) {
+      const int q = g < NA ? g : g - NA - NCH;
+      const int nk = min(KPS, KT - q * KPS);
+      const u16* src = (g < NA ? a.wo : a.wp) + (long)q * KPS * W2IMG * 8;
+      for (int u = wid; u < nk * UW2; u += 8) glds16(src + ((long)u * 64 + lane) * 8, dst + u * 64);
+    } else {
+      const int c = g - NA;
+#pragma unroll
+      for (int p = 0; p < PW1; ++p) {
+        const int q = p * 512 + tid, r = (q >> 3) & 63, pc = q & 7;
+        const int lc = pc ^ ((r >> 1) & 7);
+        glds16(a.w1 + (long)(c * 64 + r) * C + p * 64 + lc * 8, dst + p * 512 + wid * 64);
+      }
+      for (int u = wid; u < UW2; u += 8) glds16(a.w2 + ((long)c * W2IMG + u * 64 + lane) * 8, dst + WIMG + u * 64);
+    }
+  };
+  auto top = [&](int g) __attribute__((always_inline)) {  // chunk g's DMA landed everywhere; the other stage is free: refill it
+    wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (g + 1 < 2 * NA + NCH) issue(g + 1, (g + 1) & 1);
+    return (const uint4*)(lds + (g & 1) * STAGE);
+  };
+  issue(0, 0);
+
+  const int p2 = lg ^ (((l16 >> 3) & 1) << 1);  // this lane's physical piece of a [C][32] image
+  bf16x8 ar[KT];    // the B operand of the current phase: o rows, LN(h2), y
+  f32x4 out[NT2];   // C^T accumulators: out[t][r] = column 16 t + 4 lg + r of row l16
+  auto init_cols = [&](const float* v) __attribute__((always_inline)) {
+#pragma unroll
+    for (int t = 0; t < NT2; ++t) {
+      const float4 b = *(const float4*)(v + 16 * t + 4 * lg);
+      out[t] = (f32x4){b.x, b.y, b.z, b.w};
+    }
+  };
+  // GEMM0 / GEMM3 over the NA stages of a [C][C] weight, operand ar (compile-time k-steps)
+  auto proj = [&](int g0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < NA; ++q) {
+      const uint4* cur = top(g0 + q);
+      const int nk = (q + 1) * KPS <= KT ? KPS : KT - q * KPS;
+      // per-image lane offsets, laundered so that the two projections' (same-valued) LDS
+      // addresses are not shared across the FeedForward loop (kept live there, they spilled);
+      // a tile's offset within an image is an instruction immediate
+      int lo[KPS];
+#pragma unroll
+      for (int j = 0; j < KPS; ++j) {
+        lo[j] = j * W2IMG + l16 * 4 + p2;
+        asm volatile("" : "+v"(lo[j]));
+      }
+      uint4 wq[PD2];
+#pragma unroll
+      for (int i = 0; i < PD2; ++i) wq[i] = cur[lo[i / NT2] + (i % NT2) * 64];
+#pragma unroll
+      for (int j = 0; j < KPS; ++j) {
+        if (j < nk) {
+#pragma unroll
+          for (int t = 0; t < NT2; ++t) {
+            const int i = j * NT2 + t;
+            const bf16x8 wv = __builtin_bit_cast(bf16x8, wq[i % PD2]);
+            const int n = i + PD2;
+            if (n < nk * NT2) wq[i % PD2] = cur[lo[n / NT2 < KPS ? n / NT2 : 0] + (n % NT2) * 64];
+            out[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, ar[q * KPS + j < KT ? q * KPS + j : 0], out[t], 0, 0, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);  // one k-step at a time: hoisted fragment reads spill
+        }
+      }
+    }
+  };
+  // accumulators (bf16-rounded values) -> the operand registers in accumulator k order
+  auto acc_to_operand = [&](float mean, float rstd) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < KT; ++s) {
+      bf16x8 v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (__bf16)((out[2 * s + (e >> 2)][e & 3] - mean) * rstd);
+      ar[s] = v;
+    }
+  };
+
+  // ---- phase A: h2 = o Wo^T + bo + h1 ----
+  uint2 xr[NT2];  // a residual in accumulator layout: h1 in phase A, xb in phase C
+  {
+    const u16* src = a.o + row * a.ldo + lg * 8;
+#pragma unroll
+    for (int s = 0; s < KT; ++s) ar[s] = *(const bf16x8*)(src + s * 32);
+  }
+  init_cols(a.bo);
+  proj(0);
+  {
+    const u16* hr = a.h1 + row * a.ldh + 4 * lg;
+#pragma unroll
+    for (int t = 0; t < NT2; ++t) xr[t] = *(const uint2*)(hr + 16 * t);
+  }
+  float mean, rstd;
+  {
+    float s1 = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT2; ++t) {
+      const uint2 rs = xr[t];
+      const uint32_t pk0 = pack2(out[t][0] + __uint_as_float(rs.x << 16), out[t][1] + __uint_as_float(rs.x & 0xffff0000u));
+      const uint32_t pk1 = pack2(out[t][2] + __uint_as_float(rs.y << 16), out[t][3] + __uint_as_float(rs.y & 0xffff0000u));
+      out[t] = (f32x4){__uint_as_float(pk0 << 16), __uint_as_float(pk0 & 0xffff0000u),
+                       __uint_as_float(pk1 << 16), __uint_as_float(pk1 & 0xffff0000u)};
+      s1 += (out[t][0] + out[t][1]) + (out[t][2] + out[t][3]);
+    }
+    mean = xor16_32_sum(s1) * (1.0f / C);
+    float s2 = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float d = out[t][r] - mean;
+        s2 = fmaf(d, d, s2);
+      }
+    rstd = rsqrtf(xor16_32_sum(s2) * (1.0f / C) + a.eps);
+  }
+  acc_to_operand(mean, rstd);  // LN(h2), gamma / beta folded into W1 / b1
+#pragma unroll
+  for (int t = 0; t < NT2; ++t) {  // the FeedForward's accumulators start at its residual + b2
+    const float4 b = *(const float4*)(a.b2 + 16 * t + 4 * lg);
+    out[t][0] += b.x; out[t][1] += b.y; out[t][2] += b.z; out[t][3] += b.w;
+  }
+
+  // ---- phase B: the FeedForward (ff_fused_kernel's chunk loop) ----
+  for (int c = 0; c < NCH; ++c) {
+    const uint4* cur = top(NA + c);
+    f32x4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    auto frag = [&](int s, int t) {
+      return __builtin_bit_cast(bf16x8, cur[(s >> 1) * 512 + swz_bk<64>(t * 16 + l16, (s & 1) * 4 + lg)]);
+    };
+    const uint4* w2 = cur + WIMG;
+    bf16x8 wf[PD1][4];
+#pragma unroll
+    for (int p = 0; p < PD1; ++p)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) wf[p][t] = frag(p, t);
+    uint4 w2q[PD2];
+#pragma unroll
+    for (int s = 0; s < KT; ++s) {
+      const int sl = s % PD1;
+      bf16x8 cw[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) cw[t] = wf[sl][t];
+      if (s + PD1 < KT) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) wf[sl][t] = frag(s + PD1, t);
+      } else if (s + PD1 - KT < PD2) {
+        w2q[s + PD1 - KT] = w2[((s + PD1 - KT) * 16 + l16) * 4 + p2];
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cw[t], ar[s], acc[t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = PD1; q < PD2; ++q) w2q[q] = w2[(q * 16 + l16) * 4 + p2];
+    const float* bb = b1s + c * 64 + 4 * lg;
+    const float4 bh0 = *(const float4*)(bb), bg0 = *(const float4*)(bb + 16);
+    const float4 bh1 = *(const float4*)(bb + 32), bg1 = *(const float4*)(bb + 48);
+    const float hb0[4] = {bh0.x, bh0.y, bh0.z, bh0.w}, gb0[4] = {bg0.x, bg0.y, bg0.z, bg0.w};
+    const float hb1[4] = {bh1.x, bh1.y, bh1.z, bh1.w}, gb1[4] = {bg1.x, bg1.y, bg1.z, bg1.w};
+    bf16x8 gv;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      gv[r] = (__bf16)((acc[0][r] + hb0[r]) * gelu_erf(acc[1][r] + gb0[r]));
+      gv[4 + r] = (__bf16)((acc[2][r] + hb1[r]) * gelu_erf(acc[3][r] + gb1[r]));
+    }
+#pragma unroll
+    for (int t = 0; t < NT2; ++t) {
+      const bf16x8 wv = __builtin_bit_cast(bf16x8, w2q[t % PD2]);
+      if (t + PD2 < NT2) w2q[t % PD2] = w2[((t + PD2) * 16 + l16) * 4 + p2];
+      out[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, gv, out[t], 0, 0, 0);
+    }
+  }
+
+  // ---- phase C: z = y Wp^T + bp + xb ----
+  acc_to_operand(0.f, 1.f);  // y, rounded to bf16 as the unfused path stores it
+  init_cols(a.bp);
+  proj(NA + NCH);
+  {  // the residual xb
+    const u16* src = a.xb + row * a.ldxb + 4 * lg;
+#pragma unroll
+    for (int t = 0; t < NT2; ++t) xr[t] = *(const uint2*)(src + 16 * t);
+  }
+
+  // ---- epilogue: the block's 128 x C result through LDS: row stores + column sums ----
+  __syncthreads();  // every wave is past its last stage reads
+  u16* zimg = (u16*)lds;
+#pragma unroll
+  for (int t = 0; t < NT2; ++t) {
+    const uint2 rs = xr[t];
+    const float o0 = out[t][0] + __uint_as_float(rs.x << 16), o1 = out[t][1] + __uint_as_float(rs.x & 0xffff0000u);
+    const float o2 = out[t][2] + __uint_as_float(rs.y << 16), o3 = out[t][3] + __uint_as_float(rs.y & 0xffff0000u);
+    *(uint2*)(zimg + (wid * 16 + l16) * ZP + 16 * t + 4 * lg) = make_uint2(pack2(o0, o1), pack2(o2, o3));
+  }
+  __syncthreads();
+  constexpr int PCS = C / 8;  // 16-B pieces per row
+  for (int q = tid; q < 128 * PCS; q += 512) {
+    const int r = q / PCS, ch = q - r * PCS;
+    *(uint4*)(a.z + (row0 + r) * a.ldz + ch * 8) = *(const uint4*)(zimg + r * ZP + ch * 8);
+  }
+  if (a.cs_out) {
+    float* part = (float*)(zimg + 128 * ZP);  // [4 row groups][C / 4 quads][8]
+    if (tid < C) {  // thread: columns 4 cq .. + 3 over rows 32 rg .. + 31
+      const int cq = tid % (C / 4), rg = tid / (C / 4);
+      float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int r = 0; r < 32; ++r) {
+        const uint2 v = *(const uint2*)(zimg + (32 * rg + r) * ZP + 4 * cq);
+        const float f[4] = {__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u),
+                            __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xffff0000u)};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { s1[e] += f[e]; s2[e] = fmaf(f[e], f[e], s2[e]); }
+      }
+      float4* pp = (float4*)(part + (rg * (C / 4) + cq) * 8);
+      pp[0] = make_float4(s1[0], s1[1], s1[2], s1[3]);
+      pp[1] = make_float4(s2[0], s2[1], s2[2], s2[3]);
+    }
+    __syncthreads();
+    if (tid < C) {
+      const int cq = tid >> 2, e = tid & 3;
+      float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        t1 += part[(rg * (C / 4) + cq) * 8 + e];
+        t2 += part[(rg * (C / 4) + cq) * 8 + 4 + e];
+      }
+      a.cs_out[(long)blockIdx.x * 2 * C + tid] = t1;
+      a.cs_out[(long)blockIdx.x * 2 * C + C + tid] = t2;
     }
   }
 }
@@ -375,6 +692,32 @@ __global__ void __launch_bounds__(512, 1) ff_pair_kernel(FFArgs a) {
 }  // namespace ls
 
 using namespace ls;
+
+extern "C" int ls_ff_chain(const ls_ff_chain_desc* d, void* stream) {
+  if (!d || !d->o || !d->wo || !d->bo || !d->h1 || !d->w1 || !d->b1 || !d->w2 || !d->b2 || !d->wp || !d->bp ||
+      !d->xb || !d->z)
+    return fail(LS_ERR_INVALID, "ls_ff_chain: null pointer");
+  if (d->C != 320 || d->inner != 1280) return fail(LS_ERR_INVALID, "ls_ff_chain: C = 320, inner = 1280 only");
+  if (d->M <= 0 || d->M % 128 || (d->M / 128) > 0x7fffffffL)
+    return fail(LS_ERR_INVALID, "ls_ff_chain: M a positive multiple of 128");
+  if (d->ldo < d->C || d->ldh < d->C || d->ldxb < d->C || d->ldz < d->C || d->ldo % 8 || d->ldh % 4 ||
+      d->ldxb % 4 || d->ldz % 8)
+    return fail(LS_ERR_INVALID, "ls_ff_chain: pitches >= C (o, z: % 8; h1, xb: % 4)");
+  if ((((uintptr_t)d->o | (uintptr_t)d->wo | (uintptr_t)d->w1 | (uintptr_t)d->w2 | (uintptr_t)d->wp |
+        (uintptr_t)d->b1 | (uintptr_t)d->b2 | (uintptr_t)d->bo | (uintptr_t)d->bp | (uintptr_t)d->z |
+        (uintptr_t)d->cs_out) & 15) || (((uintptr_t)d->h1 | (uintptr_t)d->xb) & 7))
+    return fail(LS_ERR_INVALID, "ls_ff_chain: operands 16-B aligned (h1 / xb 8-B)");
+  FFChainArgs a;
+  a.o = (const u16*)d->o; a.wo = (const u16*)d->wo; a.bo = d->bo; a.h1 = (const u16*)d->h1;
+  a.w1 = (const u16*)d->w1; a.b1 = d->b1; a.w2 = (const u16*)d->w2; a.b2 = d->b2;
+  a.wp = (const u16*)d->wp; a.bp = d->bp; a.xb = (const u16*)d->xb; a.z = (u16*)d->z; a.cs_out = d->cs_out;
+  a.M = d->M; a.ldo = d->ldo; a.ldh = d->ldh; a.ldxb = d->ldxb; a.ldz = d->ldz; a.eps = d->eps;
+  constexpr int C = 320, I = 1280;
+  const size_t shm = (size_t)2 * (64 * (C / 64) * 8 + C * 4) * 16 + 2 * I * sizeof(float);
+  LS_SET_MAX_DYN_SHM((ff_chain_kernel<C, I>), (int)shm);
+  ff_chain_kernel<C, I><<<(unsigned)(d->M / 128), 512, shm, (hipStream_t)stream>>>(a);
+  return check_launch("ff_chain_kernel");
+}
 
 extern "C" int ls_feedforward(const ls_ff_desc* d, void* stream) {
   if (!d || !d->x || !d->ln_rowstats || !d->w1 || !d->b1 || !d->w2 || !d->b2 || !d->y)

@@ -341,6 +341,54 @@ def feedforward(x2d, ln_stats, w1: "Packed", w2: "Packed", w2ff, out=None):
     return out
 
 
+class FFChainPack:
+    """ls_ff_chain operands of one block tail (packing.pack_ff_chain): to_out, the
+    LN-folded GEGLU W1 (k permuted), W2 (pack_ff_w2), proj_out (k permuted)."""
+
+    def __init__(self, wo, bo, w1, b1, w2, b2, wp, bp, C, inner, eps):
+        self.wo, self.bo, self.w1, self.b1, self.w2, self.b2, self.wp, self.bp = wo, bo, w1, b1, w2, b2, wp, bp
+        self.C, self.inner, self.eps = C, inner, eps
+
+
+def pack_ff_chain(wo: "Packed", ff1: "Packed", ff2: "Packed", po: "Packed", eps=1e-5):
+    """FFChainPack from the packed operands of the unfused path: to_out (C, C) + bias, the
+    LN-folded GEGLU W1 (interleaved, gamma folded) + bias, W2 + bias, proj_out + bias."""
+    from .packing import pack_ff_w2, permute_k_acc
+    Cc = wo.N
+    bf = lambda t: t.to(torch.bfloat16).contiguous()
+    w1 = permute_k_acc(ff1.w.float())
+    return FFChainPack(bf(pack_ff_w2(wo.w.float()[:, :Cc], permute=False)), wo.bias.float().contiguous(), bf(w1),
+                       ff1.bias.float().contiguous(), bf(pack_ff_w2(ff2.w.float()[:, :ff2.K])),
+                       ff2.bias.float().contiguous(), bf(pack_ff_w2(po.w.float()[:, :Cc])),
+                       po.bias.float().contiguous(), Cc, ff1.N // 2, eps)
+
+
+def ff_chain_ok(o2d, pk: "FFChainPack"):
+    return (pk is not None and o2d.shape[1] == 320 and pk.inner == 1280 and o2d.shape[0] % 128 == 0
+            and o2d.stride(1) == 1 and o2d.stride(0) % 8 == 0)
+
+
+def ff_chain(o2d, h1, xb, pk: "FFChainPack", shape=None, gn_out=True):
+    """z = proj_out(FF(LN(h2)) + h2) + xb with h2 = to_out(o) + h1, one launch (ls_ff_chain);
+    o2d / h1 / xb (M, C) rows; z is allocated with `shape` (default (M, C)) and carries
+    .gn_cs (its GroupNorm column sums) for group_norm()."""
+    lib = _lib.load()
+    M, C_ = o2d.shape
+    res = torch.empty(shape or (M, C_), dtype=torch.bfloat16, device=o2d.device)
+    out = res.view(M, C_)
+    cs = torch.empty((M // GN_SLOT_ROWS, 2, C_), dtype=torch.float32, device=o2d.device) if gn_out else None
+    d = _lib.FFChainDesc()
+    d.o, d.wo, d.bo, d.h1 = _p(o2d), _p(pk.wo), _p(pk.bo), _p(h1)
+    d.w1, d.b1, d.w2, d.b2, d.wp, d.bp = _p(pk.w1), _p(pk.b1), _p(pk.w2), _p(pk.b2), _p(pk.wp), _p(pk.bp)
+    d.xb, d.z, d.cs_out = _p(xb), _p(out), _p(cs)
+    d.M, d.ldo, d.ldh, d.ldxb, d.ldz = M, o2d.stride(0), h1.stride(0), xb.stride(0), out.stride(0)
+    d.C, d.inner, d.eps = C_, pk.inner, float(pk.eps)
+    check(lib.ls_ff_chain(C.byref(d), _stream()), "ls_ff_chain")
+    if cs is not None:
+        res.gn_cs = cs
+    return res
+
+
 class XAttnPack:
     """ls_cross_attention_block operands of one BasicTransformerBlock's attn2 + norm2
     (packing.pack_xattn_q / pack_xattn_wo)."""

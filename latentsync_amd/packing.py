@@ -69,14 +69,21 @@ def geglu_interleave(w1: torch.Tensor, b1: torch.Tensor):
     return w, b
 
 
-def pack_ff_w2(w2: torch.Tensor) -> torch.Tensor:
+# k-slot (lane group lg, element i) of a 32-wide k-step -> the column a lane holds there after
+# a 16x16 MFMA accumulator tile pair (columns 4 lg .. + 3 of tile 0, then of tile 1)
+ACC_K_PERM = [(4 * lg + i) if i < 4 else (16 + 4 * lg + i - 4) for lg in range(4) for i in range(8)]
+
+
+def pack_ff_w2(w2: torch.Tensor, permute: bool = True) -> torch.Tensor:
     """FeedForward W2 (C, I) -> [I/32][C][32] for ls_feedforward (include/ls_hip.h): per
     32-column chunk, k-slot (lg, i) of a row holds column i < 4 ? 4 lg + i : 16 + 4 lg + i - 4
     (the GEGLU values a lane holds after GEMM1), and the row's four 16-B pieces are stored
-    at physical piece lg ^ (((row >> 3) & 1) << 1) (conflict-free ds_read_b128)."""
+    at physical piece lg ^ (((row >> 3) & 1) << 1) (conflict-free ds_read_b128).
+    permute=False keeps the natural column order (ls_ff_chain's wo: its operand rows come
+    from memory)."""
     C, I = w2.shape
     assert I % 32 == 0
-    perm = torch.tensor([(4 * lg + i) if i < 4 else (16 + 4 * lg + i - 4) for lg in range(4) for i in range(8)])
+    perm = torch.tensor(ACC_K_PERM if permute else list(range(32)))
     w = w2.float().reshape(C, I // 32, 32)[:, :, perm]          # (C, chunk, 32 logical slots)
     w = w.reshape(C, I // 32, 4, 8)                              # (..., logical piece, 8)
     rows = torch.arange(C)
@@ -84,6 +91,14 @@ def pack_ff_w2(w2: torch.Tensor) -> torch.Tensor:
     out = torch.empty_like(w)
     out[rows[:, None], :, phys, :] = w.permute(0, 2, 1, 3)       # (C, piece, chunk, 8) scattered
     return out.permute(1, 0, 2, 3).reshape(I // 32, C, 32).contiguous()
+
+
+def permute_k_acc(w: torch.Tensor) -> torch.Tensor:
+    """Columns of a [N][K] operand (K % 32 == 0) permuted within each 32-wide k-step by
+    ACC_K_PERM: for a B operand built from MFMA accumulators in registers (ls_ff_chain's W1)."""
+    N, K = w.shape
+    assert K % 32 == 0
+    return w.reshape(N, K // 32, 32)[:, :, torch.tensor(ACC_K_PERM)].reshape(N, K).contiguous()
 
 
 def _xattn_slot_dims():

@@ -37,6 +37,9 @@ from .weights import fill_state_dict
 _FUSED_TEMPORAL = _lib.ab_switch("LS_FUSED_TEMPORAL", "1") != "0"
 # LS_FUSED_FF=0: the FeedForward as GEGLU row-block GEMM + W2 GEMM
 _FUSED_FF = _lib.ab_switch("LS_FUSED_FF", "1") != "0"
+# LS_FF_CHAIN=0: the 32x32-level block tail (to_out + LN + FeedForward + proj_out) as three
+# launches (row-block GEMM, ls_feedforward, row-block GEMM) instead of one ls_ff_chain
+_FF_CHAIN = _lib.ab_switch("LS_FF_CHAIN", "1") != "0"
 # LS_FUSED_XATTN=1: the audio cross-attention branch at C = 320 as ONE ls_cross_attention_block
 # launch instead of q GEMM + ls_attention + out GEMM.  Off by default: measured 1-2 ms per
 # 48-window step SLOWER than the three launches (profiles/r04k_step_ab.txt)
@@ -50,6 +53,13 @@ def _ff(h, st, ff1, ff2, ff2p):
         return ops.feedforward(h, st, ff1, ff2, ff2p)
     g = ops.linear(h, ff1, act=ops.ACT_GEGLU, ln_stats=st)
     return ops.linear(g, ff2, res=h)
+
+
+def _chain_pack(o, ff1, ff2, po, c):
+    """ls_ff_chain operands of a C = 320 block tail (ops.pack_ff_chain), or None."""
+    if not (_FF_CHAIN and _FUSED_FF and c == 320 and ff1.N == 2560 and ff2.N == 320 and ff2.K == 1280):
+        return None
+    return ops.pack_ff_chain(o, ff1, ff2, po)
 
 
 def _ff2_packed(dv, key):
@@ -196,6 +206,8 @@ class _Transformer:
                                 geglu=True)
         self.ff2 = dv.packed(b + ".ff.net.2.weight", b + ".ff.net.2.bias")
         self.ff2p = _ff2_packed(dv, b + ".ff.net.2.weight")
+        # attn2.to_out + norm3 + ff + proj_out in one launch at C = 320 (ls_ff_chain)
+        self.chain = _chain_pack(self.o2, self.ff1, self.ff2, self.proj_out, c) if self.has_audio else None
 
     def audio_kv(self, audio_rows):
         """The audio cross-attention k|v projection (attn2.to_k / to_v of the audio
@@ -235,6 +247,9 @@ class _Transformer:
             ops.attention(q, kv, kv[:, C:], o, batch=n, z2=1, heads=self.heads, nq=HW, nk=L, head_dim=d,
                           qs=(HW * C, 0, C, d), ks=(L * 2 * C, 0, 2 * C, d), vs=(L * 2 * C, 0, 2 * C, d),
                           os_=(HW * C, 0, C, d))
+            if ops.ff_chain_ok(o, self.chain):
+                # to_out + residual -> norm3 -> FeedForward + residual -> proj_out + the block input
+                return ops.ff_chain(o, h, x.view(rows, C), self.chain, shape=(n, H, W, C))
             h = ops.linear(o, self.o2, res=h, stats_out=st)
         return self._tail(x, h, st, n, H, W, C)
 
@@ -277,6 +292,8 @@ class _Motion:
                                 (sd[b + ".ff_norm.weight"], sd[b + ".ff_norm.bias"]), geglu=True)
         self.ff2 = dv.packed(b + ".ff.net.2.weight", b + ".ff.net.2.bias")
         self.ff2p = _ff2_packed(dv, b + ".ff.net.2.weight")
+        # the last attention block's to_out + ff_norm + ff + proj_out in one launch (ls_ff_chain)
+        self.chain = _chain_pack(self.attn[-1]["o"], self.ff1, self.ff2, self.proj_out, c) if self.attn else None
 
     def __call__(self, x, B):
         n, H, W, C = x.shape
@@ -291,7 +308,7 @@ class _Motion:
                      stats_out=lns).view(rows, C)
         o = torch.empty((rows, C), dtype=torch.bfloat16, device=x.device)
         fuse = _FUSED_TEMPORAL and ops.temporal_attention_ok(C, self.heads, F, S)
-        for a in self.attn:
+        for i, a in enumerate(self.attn):
             if fuse and a["fused"] is not None:
                 # LayerNorm (+pe) -> q|k|v -> SDPA over the frames: q|k|v never reach HBM
                 ops.temporal_attention(h, a["fused"], B, F, S, out=o)
@@ -303,6 +320,9 @@ class _Motion:
                 st = (F * S * 3 * C, 3 * C, S * 3 * C, d)
                 ops.attention(qkv, qkv[:, C:], qkv[:, 2 * C:], o, batch=B * S, z2=S, heads=self.heads, nq=F, nk=F,
                               head_dim=d, qs=st, ks=st, vs=st, os_=(F * S * C, C, S * C, d))
+            if i == len(self.attn) - 1 and ops.ff_chain_ok(o, self.chain):
+                # to_out + residual -> ff_norm -> FeedForward + residual -> proj_out + the module input
+                return ops.ff_chain(o, h, x.view(rows, C), self.chain, shape=(n, H, W, C))
             h = ops.linear(o, a["o"], res=h, stats_out=lns)
         h = _ff(h, lns, self.ff1, self.ff2, self.ff2p)
         return ops.conv(h.view(n, H, W, C), self.proj_out, res=x, gn_out=True)

@@ -87,6 +87,19 @@ def main():
                 fl = 4.0 * rows * C * C
                 nb = rows * C * 2 * 2
                 key = (n, f"rows={rows} C={C}")
+            elif n == "group_norm":
+                # the finalize reads the producer's per-128-row slot sums (2 x C fp32 per slot),
+                # not the tensor; only without them is there a read pass over x (| x2)
+                fl = 0.0
+                x, x2 = a[0], kw.get("x2")
+                pps = x.numel() // x.shape[-1] // a[5]
+                have = ops._colsums(x, pps) is not None and (x2 is None or ops._colsums(x2, pps) is not None)
+                nb = 0.0
+                for t in (x, x2):
+                    if t is not None:
+                        rows = t.numel() // t.shape[-1]
+                        nb += (rows // ops.GN_SLOT_ROWS) * 2 * t.shape[-1] * 4 if have else t.numel() * t.element_size()
+                key = (n, f"shape={tuple(x.shape)} {'slot sums' if have else 'read pass'}")
             else:
                 fl = 0.0
                 t0 = a[0] if hasattr(a[0], "numel") else None

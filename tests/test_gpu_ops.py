@@ -689,3 +689,57 @@ def test_rowblock640_affine_odd_sample_rows(gpu, fm2):
     print("row-block K=640 affine, per-sample rel_err max", max(per_sample))
     assert max(per_sample) < 1e-2
     assert rel_err(y, y_tiled) < 1e-2
+
+
+@pytest.mark.parametrize("M", [128 * 3, 65536, 786432])
+def test_ff_chain(gpu, M):
+    """ls_ff_chain: h2 = o Wo^T + bo + h1, z = (h2 + FF(LN(h2))) Wp^T + bp + xb in one launch
+    (attention.py:174-199 to_out + norm3 + ff, :110-118 proj_out; motion_module.py:126-151,
+    262-313) against fp32 with the unfused path's bf16 roundings (h2, LN(h2), GEGLU, y), and
+    against the unfused GPU path (row-block to_out with row statistics, ls_feedforward,
+    row-block proj_out with GroupNorm column sums): z and its column sums.  M = 786432 is
+    the bench's 32x32 level (48 windows).  The fp32 check runs on 4096 rows."""
+    from latentsync_amd.unet import _Dev, _ff
+    from latentsync_amd.packing import pack_ff_w2
+    C, I = 320, 1280
+    g = torch.Generator().manual_seed(M)
+    r = lambda *s, sc=1.0: torch.randn(*s, generator=g) * sc
+    o = bf(r(M, C))
+    h1 = bf(r(M, C) * 2 + 0.3)
+    xb = bf(r(M, C))
+    wo, bo = r(C, C, sc=1 / math.sqrt(C)), r(C, sc=0.1)
+    gamma, beta = 1 + 0.2 * r(C), 0.1 * r(C)
+    w1, b1 = r(2 * I, C, sc=1 / math.sqrt(C)), r(2 * I, sc=0.1)
+    w2, b2 = r(C, I, sc=1 / math.sqrt(I)), r(C, sc=0.1)
+    wp, bp = r(C, C, sc=1 / math.sqrt(C)), r(C, sc=0.1)
+    dv = _Dev({"wo": wo, "bo": bo, "w2": w2, "b2": b2, "wp": wp, "bp": bp}, DEV)
+    pko, pkp, ff2 = dv.packed("wo", "bo"), dv.packed("wp", "bp"), dv.packed("w2", "b2")
+    ff1 = dv.packed_ln(w1, b1, (gamma, beta), geglu=True)
+    chain = ops.pack_ff_chain(pko, ff1, ff2, pkp)
+    od, h1d, xbd = (t.to(torch.bfloat16).to(DEV) for t in (o, h1, xb))
+    assert ops.ff_chain_ok(od, chain)
+    z = ops.ff_chain(od, h1d, xbd, chain)
+    cs = z.gn_cs
+    # unfused GPU path
+    st = torch.empty((M, 2), dtype=torch.float32, device=DEV)
+    h2 = ops.linear(od, pko, res=h1d, stats_out=st)
+    y = _ff(h2, st, ff1, ff2, pack_ff_w2(w2).to(torch.bfloat16).to(DEV))
+    z2 = ops.conv(y.view(1, 1, M, C), pkp, res=xbd.view(1, 1, M, C), gn_out=True)
+    e2 = rel_err(z.float(), z2.view(M, C).float())
+    ecs = rel_err(cs.double().sum(0), z2.gn_cs.double().sum(0))
+    print(f"ff_chain M={M}: vs unfused GPU path rel {e2:.2e}, column sums rel {ecs:.2e}")
+    assert e2 < 1e-2 and ecs < 1e-2
+    # column sums are those of the stored z (per 128-row slot)
+    zz = z.float().view(M // 128, 128, C)
+    assert torch.allclose(cs[:, 0], zz.sum(1), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(cs[:, 1], (zz * zz).sum(1), rtol=1e-3, atol=1e-1)
+    # fp32 reference with the unfused path's bf16 roundings, on the first rows
+    n = min(M, 4096)
+    h2r = bf(o[:n] @ bf(wo).T + bo + h1[:n])
+    t = bf(F.layer_norm(h2r, (C,), gamma, beta, eps=1e-5))
+    hg = t @ w1.T + b1
+    yr = bf(h2r + bf(hg[:, :I] * F.gelu(hg[:, I:])) @ w2.T + b2)
+    zr = yr @ bf(wp).T + bp + xb[:n]
+    e = rel_err(z[:n].float().cpu(), zr)
+    print(f"ff_chain M={M}: vs fp32 rel {e:.2e}")
+    assert e < 1e-2
