@@ -225,14 +225,24 @@ def step_probe(engine, device):
             blocks[-1][2] += 2.0 * M * w1.N * C + 2.0 * M * C * (w1.N // 2)
         return r
 
+    orig_chain = ops.ff_chain
+
+    def ff_chain(o2d, h1, xb, pk, **kw):
+        # fused to_out + FeedForward + proj_out (ls_ff_chain): 2*M*C*C twice + 2*M*2I*C + 2*M*C*I FLOPs
+        r = orig_chain(o2d, h1, xb, pk, **kw)
+        M, C = o2d.shape
+        if depth[0]:
+            blocks[-1][2] += 4.0 * M * C * C + 2.0 * M * 2 * pk.inner * C + 2.0 * M * C * pk.inner
+        return r
+
     ops.conv, ops.attention, ops.temporal_attention, ops.feedforward = conv, attention, temporal_attention, feedforward
-    ops.cross_attention_block = cross_attention_block
+    ops.cross_attention_block, ops.ff_chain = cross_attention_block, ff_chain
     U._Transformer.__call__, U._Motion.__call__ = wrap(orig_t), wrap(orig_m)
     try:
         engine._step()
     finally:
         ops.conv, ops.attention, ops.temporal_attention, ops.feedforward = orig_conv, orig_attn, orig_tattn, orig_ff
-        ops.cross_attention_block = orig_xa
+        ops.cross_attention_block, ops.ff_chain = orig_xa, orig_chain
         U._Transformer.__call__, U._Motion.__call__ = orig_t, orig_m
     torch.cuda.synchronize(device)
 

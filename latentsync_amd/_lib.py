@@ -168,6 +168,11 @@ def load(path: str = None):
         fn.argtypes = args
     if lib.ls_abi_version() != ABI_VERSION:
         raise RuntimeError(f"libls_hip.so ABI {lib.ls_abi_version()} != {ABI_VERSION}; rebuild it")
+    # diagnostics A/B runs: LS_TUNE="key=value,..." applied through ls_set_tuning
+    for kv in filter(None, ab_switch("LS_TUNE", "").split(",")):
+        k, v = (int(t) for t in kv.split("="))
+        if lib.ls_set_tuning(k, v) != 0:
+            raise RuntimeError(f"LS_TUNE {kv}: {lib.ls_last_error().decode()}")
     _lib = lib
     return lib
 

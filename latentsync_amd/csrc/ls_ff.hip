@@ -236,8 +236,15 @@ struct FFChainArgs {
   float eps;          // the LayerNorm's eps
 };
 
-template <int C, int I>
-__global__ void __launch_bounds__(512, 1) ff_chain_kernel(FFChainArgs a) {
+// FMR = 16-row fragments per wave: 1 -> 8 waves of 16 rows (two per SIMD, <= 256 registers);
+// 2 -> 4 waves of 32 rows, one per SIMD (up to 512 registers, the accumulators in AGPRs):
+// every W fragment read from LDS then feeds two MFMAs -- at one fragment per MFMA the
+// FeedForward's fragment reads alone fill the LDS array (1 KB per 16-cycle MFMA per SIMD =
+// 256 B/clk/CU), which had left it at 0.34 of the MFMA peak.
+template <int C, int I, int FMR>
+__global__ void __launch_bounds__(512 / FMR, 1) ff_chain_kernel(FFChainArgs a) {
+  constexpr int NW = 8 / FMR;             // waves per block (128 rows)
+  constexpr int NT = 64 * NW;
   constexpr int KT = C / 32;              // k-steps of every C-wide contraction
   constexpr int NCH = I / 32;             // FeedForward inner chunks
   constexpr int WIMG = 64 * (C / 64) * 8; // uint4: W1 chunk
@@ -246,42 +253,44 @@ __global__ void __launch_bounds__(512, 1) ff_chain_kernel(FFChainArgs a) {
   constexpr int KPS = STAGE / W2IMG;      // k-step images per stage in phases A / C
   constexpr int NA = (KT + KPS - 1) / KPS;  // stages of phase A (and of phase C)
   constexpr int NT2 = C / 16;             // output tiles
-  constexpr int PW1 = WIMG / 512;
+  constexpr int PW1 = WIMG / NT;
   constexpr int UW2 = W2IMG / 64;
   constexpr int PD1 = 2, PD2 = 6;
   constexpr int ZP = C + 8;               // LDS pitch (bf16) of the block's result image
-  static_assert(STAGE % W2IMG == 0 && KPS >= 1 && 2 * STAGE * 16 >= 128 * ZP * 2 + 4 * 80 * 8 * 4, "ff_chain LDS");
-  static_assert(C == 320 && I == 1280, "ff_chain shape");
+  constexpr int RG = NT >= C ? 4 : 2;     // row groups of the column-sum pass
+  static_assert(STAGE % W2IMG == 0 && KPS >= 1 && WIMG % NT == 0, "ff_chain stage layout");
+  static_assert(2 * STAGE * 16 >= 128 * ZP * 2 + RG * (C / 4) * 8 * 4, "ff_chain epilogue LDS");
+  static_assert(C == 320 && I == 1280 && (FMR == 1 || FMR == 2), "ff_chain shape");
   extern __shared__ __attribute__((aligned(16))) uint4 lds[];  // [2][STAGE], then b1 (2I fp32)
   float* b1s = (float*)(lds + 2 * STAGE);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, lg = lane >> 4;
   const long row0 = (long)blockIdx.x * 128;
-  const long row = row0 + wid * 16 + l16;  // host: M % 128 == 0
+  const int wr0 = wid * 16 * FMR + l16;   // block row of fragment 0 (fragment f: + 16 f); host: M % 128 == 0
 
-  for (int i = tid; i < 2 * I / 4; i += 512) ((float4*)b1s)[i] = ((const float4*)a.b1)[i];
+  for (int i = tid; i < 2 * I / 4; i += NT) ((float4*)b1s)[i] = ((const float4*)a.b1)[i];
 
   // chunk g of the launch: [0, NA) Wo stages, [NA, NA + NCH) FeedForward chunks, then Wp stages
-  auto issue = [&](int g, int st) {
+  auto issue = [&](int g, int st) __attribute__((always_inline)) {
     uint4* dst = lds + st * STAGE;
     if (g < NA || g >= NA + NCH) {
       const int q = g < NA ? g : g - NA - NCH;
       const int nk = min(KPS, KT - q * KPS);
       const u16* src = (g < NA ? a.wo : a.wp) + (long)q * KPS * W2IMG * 8;
-      for (int u = wid; u < nk * UW2; u += 8) glds16(src + ((long)u * 64 + lane) * 8, dst + u * 64);
+      for (int u = wid; u < nk * UW2; u += NW) glds16(src + ((long)u * 64 + lane) * 8, dst + u * 64);
     } else {
       const int c = g - NA;
 #pragma unroll
-      for (int p = 0; p < PW1; ++p) {
-        const int q = p * 512 + tid, r = (q >> 3) & 63, pc = q & 7;
+      for (int p = 0; p < PW1; ++p) {  // piece q: image q >> 9, row (q >> 3) & 63, physical chunk q & 7
+        const int q = p * NT + tid, r = (q >> 3) & 63, pc = q & 7;
         const int lc = pc ^ ((r >> 1) & 7);
-        glds16(a.w1 + (long)(c * 64 + r) * C + p * 64 + lc * 8, dst + p * 512 + wid * 64);
+        glds16(a.w1 + (long)(c * 64 + r) * C + (q >> 9) * 64 + lc * 8, dst + p * NT + wid * 64);
       }
-      for (int u = wid; u < UW2; u += 8) glds16(a.w2 + ((long)c * W2IMG + u * 64 + lane) * 8, dst + WIMG + u * 64);
+      for (int u = wid; u < UW2; u += NW) glds16(a.w2 + ((long)c * W2IMG + u * 64 + lane) * 8, dst + WIMG + u * 64);
     }
   };
-  auto top = [&](int g) __attribute__((always_inline)) {  // chunk g's DMA landed everywhere; the other stage is free: refill it
+  auto top = [&](int g) __attribute__((always_inline)) {  // chunk g's DMA landed everywhere; refill the other stage
     wait_vm<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -292,13 +301,14 @@ __global__ void __launch_bounds__(512, 1) ff_chain_kernel(FFChainArgs a) {
   issue(0, 0);
 
   const int p2 = lg ^ (((l16 >> 3) & 1) << 1);  // this lane's physical piece of a [C][32] image
-  bf16x8 ar[KT];    // the B operand of the current phase: o rows, LN(h2), y
-  f32x4 out[NT2];   // C^T accumulators: out[t][r] = column 16 t + 4 lg + r of row l16
+  bf16x8 ar[FMR][KT];   // the B operand of the current phase: o rows, LN(h2), y
+  f32x4 out[FMR][NT2];  // C^T accumulators: out[f][t][r] = column 16 t + 4 lg + r of row 16 f + l16
   auto init_cols = [&](const float* v) __attribute__((always_inline)) {
 #pragma unroll
     for (int t = 0; t < NT2; ++t) {
       const float4 b = *(const float4*)(v + 16 * t + 4 * lg);
-      out[t] = (f32x4){b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int f = 0; f < FMR; ++f) out[f][t] = (f32x4){b.x, b.y, b.z, b.w};
     }
   };
   // GEMM0 / GEMM3 over the NA stages of a [C][C] weight, operand ar (compile-time k-steps)
@@ -322,13 +332,16 @@ __global__ void __launch_bounds__(512, 1) ff_chain_kernel(FFChainArgs a) {
 #pragma unroll
       for (int j = 0; j < KPS; ++j) {
         if (j < nk) {
+          const int k = q * KPS + j < KT ? q * KPS + j : 0;
 #pragma unroll
           for (int t = 0; t < NT2; ++t) {
             const int i = j * NT2 + t;
             const bf16x8 wv = __builtin_bit_cast(bf16x8, wq[i % PD2]);
             const int n = i + PD2;
             if (n < nk * NT2) wq[i % PD2] = cur[lo[n / NT2 < KPS ? n / NT2 : 0] + (n % NT2) * 64];
-            out[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, ar[q * KPS + j < KT ? q * KPS + j : 0], out[t], 0, 0, 0);
+#pragma unroll
+            for (int f = 0; f < FMR; ++f)
+              out[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, ar[f][k], out[f][t], 0, 0, 0);
           }
           __builtin_amdgcn_sched_barrier(0);  // one k-step at a time: hoisted fragment reads spill
         }
@@ -336,66 +349,70 @@ __global__ void __launch_bounds__(512, 1) ff_chain_kernel(FFChainArgs a) {
     }
   };
   // accumulators (bf16-rounded values) -> the operand registers in accumulator k order
-  auto acc_to_operand = [&](float mean, float rstd) __attribute__((always_inline)) {
+  auto acc_to_operand = [&](int f, float mean, float rstd) __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < KT; ++s) {
       bf16x8 v;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = (__bf16)((out[2 * s + (e >> 2)][e & 3] - mean) * rstd);
-      ar[s] = v;
+      for (int e = 0; e < 8; ++e) v[e] = (__bf16)((out[f][2 * s + (e >> 2)][e & 3] - mean) * rstd);
+      ar[f][s] = v;
     }
   };
 
   // ---- phase A: h2 = o Wo^T + bo + h1 ----
-  uint2 xr[NT2];  // a residual in accumulator layout: h1 in phase A, xb in phase C
-  {
-    const u16* src = a.o + row * a.ldo + lg * 8;
 #pragma unroll
-    for (int s = 0; s < KT; ++s) ar[s] = *(const bf16x8*)(src + s * 32);
+  for (int f = 0; f < FMR; ++f) {
+    const u16* src = a.o + (row0 + wr0 + 16 * f) * a.ldo + lg * 8;
+#pragma unroll
+    for (int s = 0; s < KT; ++s) ar[f][s] = *(const bf16x8*)(src + s * 32);
   }
   init_cols(a.bo);
   proj(0);
-  {
-    const u16* hr = a.h1 + row * a.ldh + 4 * lg;
+#pragma unroll
+  for (int f = 0; f < FMR; ++f) {
+    uint2 xr[NT2];
+    const u16* hr = a.h1 + (row0 + wr0 + 16 * f) * a.ldh + 4 * lg;
 #pragma unroll
     for (int t = 0; t < NT2; ++t) xr[t] = *(const uint2*)(hr + 16 * t);
-  }
-  float mean, rstd;
-  {
     float s1 = 0.f;
 #pragma unroll
     for (int t = 0; t < NT2; ++t) {
       const uint2 rs = xr[t];
-      const uint32_t pk0 = pack2(out[t][0] + __uint_as_float(rs.x << 16), out[t][1] + __uint_as_float(rs.x & 0xffff0000u));
-      const uint32_t pk1 = pack2(out[t][2] + __uint_as_float(rs.y << 16), out[t][3] + __uint_as_float(rs.y & 0xffff0000u));
-      out[t] = (f32x4){__uint_as_float(pk0 << 16), __uint_as_float(pk0 & 0xffff0000u),
-                       __uint_as_float(pk1 << 16), __uint_as_float(pk1 & 0xffff0000u)};
-      s1 += (out[t][0] + out[t][1]) + (out[t][2] + out[t][3]);
+      const uint32_t pk0 = pack2(out[f][t][0] + __uint_as_float(rs.x << 16), out[f][t][1] + __uint_as_float(rs.x & 0xffff0000u));
+      const uint32_t pk1 = pack2(out[f][t][2] + __uint_as_float(rs.y << 16), out[f][t][3] + __uint_as_float(rs.y & 0xffff0000u));
+      out[f][t] = (f32x4){__uint_as_float(pk0 << 16), __uint_as_float(pk0 & 0xffff0000u),
+                          __uint_as_float(pk1 << 16), __uint_as_float(pk1 & 0xffff0000u)};
+      s1 += (out[f][t][0] + out[f][t][1]) + (out[f][t][2] + out[f][t][3]);
     }
-    mean = xor16_32_sum(s1) * (1.0f / C);
+    const float mean = xor16_32_sum(s1) * (1.0f / C);
     float s2 = 0.f;
 #pragma unroll
     for (int t = 0; t < NT2; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float d = out[t][r] - mean;
+        const float d = out[f][t][r] - mean;
         s2 = fmaf(d, d, s2);
       }
-    rstd = rsqrtf(xor16_32_sum(s2) * (1.0f / C) + a.eps);
+    const float rstd = rsqrtf(xor16_32_sum(s2) * (1.0f / C) + a.eps);
+    acc_to_operand(f, mean, rstd);  // LN(h2), gamma / beta folded into W1 / b1
   }
-  acc_to_operand(mean, rstd);  // LN(h2), gamma / beta folded into W1 / b1
 #pragma unroll
   for (int t = 0; t < NT2; ++t) {  // the FeedForward's accumulators start at its residual + b2
     const float4 b = *(const float4*)(a.b2 + 16 * t + 4 * lg);
-    out[t][0] += b.x; out[t][1] += b.y; out[t][2] += b.z; out[t][3] += b.w;
+#pragma unroll
+    for (int f = 0; f < FMR; ++f) {
+      out[f][t][0] += b.x; out[f][t][1] += b.y; out[f][t][2] += b.z; out[f][t][3] += b.w;
+    }
   }
 
   // ---- phase B: the FeedForward (ff_fused_kernel's chunk loop) ----
   for (int c = 0; c < NCH; ++c) {
     const uint4* cur = top(NA + c);
-    f32x4 acc[4];
+    f32x4 acc[FMR][4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int f = 0; f < FMR; ++f)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[f][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
     auto frag = [&](int s, int t) {
       return __builtin_bit_cast(bf16x8, cur[(s >> 1) * 512 + swz_bk<64>(t * 16 + l16, (s & 1) * 4 + lg)]);
     };
@@ -419,7 +436,9 @@ __global__ void __launch_bounds__(512, 1) ff_chain_kernel(FFChainArgs a) {
         w2q[s + PD1 - KT] = w2[((s + PD1 - KT) * 16 + l16) * 4 + p2];
       }
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cw[t], ar[s], acc[t], 0, 0, 0);
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int f = 0; f < FMR; ++f) acc[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cw[t], ar[f][s], acc[f][t], 0, 0, 0);
     }
 #pragma unroll
     for (int q = PD1; q < PD2; ++q) w2q[q] = w2[(q * 16 + l16) * 4 + p2];
@@ -428,73 +447,80 @@ __global__ void __launch_bounds__(512, 1) ff_chain_kernel(FFChainArgs a) {
     const float4 bh1 = *(const float4*)(bb + 32), bg1 = *(const float4*)(bb + 48);
     const float hb0[4] = {bh0.x, bh0.y, bh0.z, bh0.w}, gb0[4] = {bg0.x, bg0.y, bg0.z, bg0.w};
     const float hb1[4] = {bh1.x, bh1.y, bh1.z, bh1.w}, gb1[4] = {bg1.x, bg1.y, bg1.z, bg1.w};
-    bf16x8 gv;
+    bf16x8 gv[FMR];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      gv[r] = (__bf16)((acc[0][r] + hb0[r]) * gelu_erf(acc[1][r] + gb0[r]));
-      gv[4 + r] = (__bf16)((acc[2][r] + hb1[r]) * gelu_erf(acc[3][r] + gb1[r]));
-    }
+    for (int f = 0; f < FMR; ++f)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        gv[f][r] = (__bf16)((acc[f][0][r] + hb0[r]) * gelu_erf(acc[f][1][r] + gb0[r]));
+        gv[f][4 + r] = (__bf16)((acc[f][2][r] + hb1[r]) * gelu_erf(acc[f][3][r] + gb1[r]));
+      }
 #pragma unroll
     for (int t = 0; t < NT2; ++t) {
       const bf16x8 wv = __builtin_bit_cast(bf16x8, w2q[t % PD2]);
       if (t + PD2 < NT2) w2q[t % PD2] = w2[((t + PD2) * 16 + l16) * 4 + p2];
-      out[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, gv, out[t], 0, 0, 0);
+#pragma unroll
+      for (int f = 0; f < FMR; ++f) out[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, gv[f], out[f][t], 0, 0, 0);
     }
   }
 
   // ---- phase C: z = y Wp^T + bp + xb ----
-  acc_to_operand(0.f, 1.f);  // y, rounded to bf16 as the unfused path stores it
+#pragma unroll
+  for (int f = 0; f < FMR; ++f) acc_to_operand(f, 0.f, 1.f);  // y, rounded to bf16 as the unfused path stores it
   init_cols(a.bp);
   proj(NA + NCH);
-  {  // the residual xb
-    const u16* src = a.xb + row * a.ldxb + 4 * lg;
-#pragma unroll
-    for (int t = 0; t < NT2; ++t) xr[t] = *(const uint2*)(src + 16 * t);
-  }
 
-  // ---- epilogue: the block's 128 x C result through LDS: row stores + column sums ----
+  // ---- epilogue: + xb, the block's 128 x C result through LDS: row stores + column sums ----
   __syncthreads();  // every wave is past its last stage reads
   u16* zimg = (u16*)lds;
 #pragma unroll
-  for (int t = 0; t < NT2; ++t) {
-    const uint2 rs = xr[t];
-    const float o0 = out[t][0] + __uint_as_float(rs.x << 16), o1 = out[t][1] + __uint_as_float(rs.x & 0xffff0000u);
-    const float o2 = out[t][2] + __uint_as_float(rs.y << 16), o3 = out[t][3] + __uint_as_float(rs.y & 0xffff0000u);
-    *(uint2*)(zimg + (wid * 16 + l16) * ZP + 16 * t + 4 * lg) = make_uint2(pack2(o0, o1), pack2(o2, o3));
+  for (int f = 0; f < FMR; ++f) {
+    uint2 xr[NT2];
+    const u16* src = a.xb + (row0 + wr0 + 16 * f) * a.ldxb + 4 * lg;
+#pragma unroll
+    for (int t = 0; t < NT2; ++t) xr[t] = *(const uint2*)(src + 16 * t);
+#pragma unroll
+    for (int t = 0; t < NT2; ++t) {
+      const uint2 rs = xr[t];
+      const float o0 = out[f][t][0] + __uint_as_float(rs.x << 16), o1 = out[f][t][1] + __uint_as_float(rs.x & 0xffff0000u);
+      const float o2 = out[f][t][2] + __uint_as_float(rs.y << 16), o3 = out[f][t][3] + __uint_as_float(rs.y & 0xffff0000u);
+      *(uint2*)(zimg + (wr0 + 16 * f) * ZP + 16 * t + 4 * lg) = make_uint2(pack2(o0, o1), pack2(o2, o3));
+    }
   }
   __syncthreads();
   constexpr int PCS = C / 8;  // 16-B pieces per row
-  for (int q = tid; q < 128 * PCS; q += 512) {
+  for (int q = tid; q < 128 * PCS; q += NT) {
     const int r = q / PCS, ch = q - r * PCS;
     *(uint4*)(a.z + (row0 + r) * a.ldz + ch * 8) = *(const uint4*)(zimg + r * ZP + ch * 8);
   }
   if (a.cs_out) {
-    float* part = (float*)(zimg + 128 * ZP);  // [4 row groups][C / 4 quads][8]
-    if (tid < C) {  // thread: columns 4 cq .. + 3 over rows 32 rg .. + 31
+    constexpr int RPG = 128 / RG;  // rows per group
+    float* part = (float*)(zimg + 128 * ZP);  // [RG row groups][C / 4 quads][8]
+    if (tid < RG * (C / 4)) {  // thread: columns 4 cq .. + 3 over rows RPG rg .. + RPG - 1
       const int cq = tid % (C / 4), rg = tid / (C / 4);
       float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int r = 0; r < 32; ++r) {
-        const uint2 v = *(const uint2*)(zimg + (32 * rg + r) * ZP + 4 * cq);
-        const float f[4] = {__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u),
-                            __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xffff0000u)};
+      for (int r = 0; r < RPG; ++r) {
+        const uint2 v = *(const uint2*)(zimg + (RPG * rg + r) * ZP + 4 * cq);
+        const float fv[4] = {__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u),
+                             __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xffff0000u)};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) { s1[e] += f[e]; s2[e] = fmaf(f[e], f[e], s2[e]); }
+        for (int e = 0; e < 4; ++e) { s1[e] += fv[e]; s2[e] = fmaf(fv[e], fv[e], s2[e]); }
       }
       float4* pp = (float4*)(part + (rg * (C / 4) + cq) * 8);
       pp[0] = make_float4(s1[0], s1[1], s1[2], s1[3]);
       pp[1] = make_float4(s2[0], s2[1], s2[2], s2[3]);
     }
     __syncthreads();
-    if (tid < C) {
-      const int cq = tid >> 2, e = tid & 3;
+    for (int col = tid; col < C; col += NT) {
+      const int cq = col >> 2, e = col & 3;
       float t1 = 0.f, t2 = 0.f;
 #pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
+      for (int rg = 0; rg < RG; ++rg) {
         t1 += part[(rg * (C / 4) + cq) * 8 + e];
         t2 += part[(rg * (C / 4) + cq) * 8 + 4 + e];
       }
-      a.cs_out[(long)blockIdx.x * 2 * C + tid] = t1;
-      a.cs_out[(long)blockIdx.x * 2 * C + C + tid] = t2;
+      a.cs_out[(long)blockIdx.x * 2 * C + col] = t1;
+      a.cs_out[(long)blockIdx.x * 2 * C + C + col] = t2;
     }
   }
 }
@@ -693,6 +719,9 @@ __global__ void __launch_bounds__(512, 1) ff_pair_kernel(FFArgs a) {
 
 using namespace ls;
 
+// rows per wave of ls_ff_chain: 32 (2, the default) or 16 (1) -- ls_set_tuning key 17
+int g_ff_chain_fmr = 2;
+
 extern "C" int ls_ff_chain(const ls_ff_chain_desc* d, void* stream) {
   if (!d || !d->o || !d->wo || !d->bo || !d->h1 || !d->w1 || !d->b1 || !d->w2 || !d->b2 || !d->wp || !d->bp ||
       !d->xb || !d->z)
@@ -714,8 +743,13 @@ extern "C" int ls_ff_chain(const ls_ff_chain_desc* d, void* stream) {
   a.M = d->M; a.ldo = d->ldo; a.ldh = d->ldh; a.ldxb = d->ldxb; a.ldz = d->ldz; a.eps = d->eps;
   constexpr int C = 320, I = 1280;
   const size_t shm = (size_t)2 * (64 * (C / 64) * 8 + C * 4) * 16 + 2 * I * sizeof(float);
-  LS_SET_MAX_DYN_SHM((ff_chain_kernel<C, I>), (int)shm);
-  ff_chain_kernel<C, I><<<(unsigned)(d->M / 128), 512, shm, (hipStream_t)stream>>>(a);
+  if (g_ff_chain_fmr == 1) {
+    LS_SET_MAX_DYN_SHM((ff_chain_kernel<C, I, 1>), (int)shm);
+    ff_chain_kernel<C, I, 1><<<(unsigned)(d->M / 128), 512, shm, (hipStream_t)stream>>>(a);
+  } else {
+    LS_SET_MAX_DYN_SHM((ff_chain_kernel<C, I, 2>), (int)shm);
+    ff_chain_kernel<C, I, 2><<<(unsigned)(d->M / 128), 256, shm, (hipStream_t)stream>>>(a);
+  }
   return check_launch("ff_chain_kernel");
 }
 

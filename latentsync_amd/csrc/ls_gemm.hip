@@ -2970,8 +2970,14 @@ using namespace ls;
 
 namespace ls { void attn_set_attn6(bool on); }
 
+extern int g_ff_chain_fmr;  // ls_ff.hip
+
 extern "C" int ls_set_tuning(int32_t key, int32_t value) {
   switch (key) {
+    case 17:
+      if (value != 1 && value != 2) return fail(LS_ERR_INVALID, "ls_ff_chain rows per wave: 1 (16) or 2 (32)");
+      g_ff_chain_fmr = value;
+      return LS_OK;
     case 1: g_force_regstage = value != 0; return LS_OK;
     case 2:
 #ifndef LS_DIAG_KERNELS

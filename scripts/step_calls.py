@@ -41,7 +41,7 @@ def main():
         return e
 
     names = ["conv", "attention", "group_norm", "group_norm_apply", "row_stats", "layer_norm", "feedforward",
-             "temporal_attention", "cross_attention_block", "small_linear", "ddim_cfg_step", "add_rows"]
+             "temporal_attention", "cross_attention_block", "ff_chain", "small_linear", "ddim_cfg_step", "add_rows"]
     names = [n for n in names if hasattr(ops, n)]
     orig = {n: getattr(ops, n) for n in names}
 
@@ -81,6 +81,12 @@ def main():
                 fl = 2.0 * rows * 3 * C * C + 4.0 * ns * S * pk.heads * F * F * (C // pk.heads)
                 nb = rows * C * 2 * 2
                 key = (n, f"rows={rows} C={C} F={F}")
+            elif n == "ff_chain":
+                o2d, pk = a[0], a[3]
+                rows, C = o2d.shape
+                fl = 4.0 * rows * C * C + 6.0 * rows * C * pk.inner
+                nb = rows * C * 2 * 4 + (pk.w1.numel() + pk.w2.numel() + pk.wo.numel() + pk.wp.numel()) * 2
+                key = (n, f"rows={rows} C={C} inner={pk.inner}")
             elif n == "cross_attention_block":
                 x2d = a[0]
                 rows, C = x2d.shape

@@ -691,8 +691,9 @@ def test_rowblock640_affine_odd_sample_rows(gpu, fm2):
     assert rel_err(y, y_tiled) < 1e-2
 
 
+@pytest.mark.parametrize("fmr", [2, 1])
 @pytest.mark.parametrize("M", [128 * 3, 65536, 786432])
-def test_ff_chain(gpu, M):
+def test_ff_chain(gpu, M, fmr):
     """ls_ff_chain: h2 = o Wo^T + bo + h1, z = (h2 + FF(LN(h2))) Wp^T + bp + xb in one launch
     (attention.py:174-199 to_out + norm3 + ff, :110-118 proj_out; motion_module.py:126-151,
     262-313) against fp32 with the unfused path's bf16 roundings (h2, LN(h2), GEGLU, y), and
@@ -718,7 +719,13 @@ def test_ff_chain(gpu, M):
     chain = ops.pack_ff_chain(pko, ff1, ff2, pkp)
     od, h1d, xbd = (t.to(torch.bfloat16).to(DEV) for t in (o, h1, xb))
     assert ops.ff_chain_ok(od, chain)
-    z = ops.ff_chain(od, h1d, xbd, chain)
+    from latentsync_amd import _lib
+    lib = _lib.load()
+    assert lib.ls_set_tuning(17, fmr) == 0  # rows per wave: 32 (default) / 16
+    try:
+        z = ops.ff_chain(od, h1d, xbd, chain)
+    finally:
+        lib.ls_set_tuning(17, 2)
     cs = z.gn_cs
     # unfused GPU path
     st = torch.empty((M, 2), dtype=torch.float32, device=DEV)
@@ -727,7 +734,7 @@ def test_ff_chain(gpu, M):
     z2 = ops.conv(y.view(1, 1, M, C), pkp, res=xbd.view(1, 1, M, C), gn_out=True)
     e2 = rel_err(z.float(), z2.view(M, C).float())
     ecs = rel_err(cs.double().sum(0), z2.gn_cs.double().sum(0))
-    print(f"ff_chain M={M}: vs unfused GPU path rel {e2:.2e}, column sums rel {ecs:.2e}")
+    print(f"ff_chain M={M} fmr={fmr}: vs unfused GPU path rel {e2:.2e}, column sums rel {ecs:.2e}")
     assert e2 < 1e-2 and ecs < 1e-2
     # column sums are those of the stored z (per 128-row slot)
     zz = z.float().view(M // 128, 128, C)
