@@ -405,63 +405,177 @@ __global__ void __launch_bounds__(512 / FMR, 1) ff_chain_kernel(FFChainArgs a) {
     }
   }
 
-  // ---- phase B: the FeedForward (ff_fused_kernel's chunk loop) ----
-  for (int c = 0; c < NCH; ++c) {
-    const uint4* cur = top(NA + c);
-    f32x4 acc[FMR][4];
+  // ---- phase B: the FeedForward ----
+  // GELU of the chunk's 32 inner columns from the GEMM1 accumulators (biases from LDS)
+  auto gelu_val = [&](f32x4 (&ac)[FMR][4], int c, int f, int hh, int r) __attribute__((always_inline)) {
+    const float* bb = b1s + c * 64 + 32 * hh + 4 * lg;
+    return (__bf16)((ac[f][2 * hh][r] + bb[r]) * gelu_erf(ac[f][2 * hh + 1][r] + bb[16 + r]));
+  };
+  if constexpr (FMR == 2) {
+    // One wave per SIMD, software-pipelined: iteration c runs GEMM1 of chunk c + 1 with the
+    // GELUs of chunk c between its MFMAs, then GEMM2 of chunk c -- a lone wave would
+    // otherwise wait out every MFMA -> GELU -> MFMA dependency.  W1 of chunk c sits in W1
+    // slot c & 1 (the first WIMG of stage c & 1), W2 of chunk c in W2 slot c & 1: W1 runs
+    // one chunk ahead of W2, so at barrier T(c) W1(c + 2) refills the W1 slot GEMM1(c) left and
+    // W2(c + 1) the W2 slot GEMM2(c - 1) left.  (Phase A's last barrier issued W1(0) + W2(0).)
+    auto issue_w1 = [&](int c) __attribute__((always_inline)) {
+      uint4* dst = lds + (c & 1) * STAGE;
 #pragma unroll
-    for (int f = 0; f < FMR; ++f)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) acc[f][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    auto frag = [&](int s, int t) {
-      return __builtin_bit_cast(bf16x8, cur[(s >> 1) * 512 + swz_bk<64>(t * 16 + l16, (s & 1) * 4 + lg)]);
+      for (int p = 0; p < PW1; ++p) {
+        const int q = p * NT + tid, r = (q >> 3) & 63, pc = q & 7;
+        const int lc = pc ^ ((r >> 1) & 7);
+        glds16(a.w1 + (long)(c * 64 + r) * C + (q >> 9) * 64 + lc * 8, dst + p * NT + wid * 64);
+      }
     };
-    const uint4* w2 = cur + WIMG;
-    bf16x8 wf[PD1][4];
+    auto issue_w2 = [&](int c) __attribute__((always_inline)) {
+      uint4* dst = lds + (c & 1) * STAGE + WIMG;
+      for (int u = wid; u < UW2; u += NW) glds16(a.w2 + ((long)c * W2IMG + u * 64 + lane) * 8, dst + u * 64);
+    };
+    auto bar = [&]() __attribute__((always_inline)) {
+      wait_vm<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    };
+    // GEMM1 of chunk cn into nx; with GL the GELUs of chunk cn - 1 (from cu) between its k-steps
+    auto gemm1 = [&](int cn, f32x4 (&nx)[FMR][4], f32x4 (&cu)[FMR][4], bf16x8 (&gv)[FMR], auto gl_tag)
+        __attribute__((always_inline)) {
+      constexpr bool GL = decltype(gl_tag)::value;
+      const uint4* cur = lds + (cn & 1) * STAGE;
+      auto frag = [&](int s, int t) {
+        return __builtin_bit_cast(bf16x8, cur[(s >> 1) * 512 + swz_bk<64>(t * 16 + l16, (s & 1) * 4 + lg)]);
+      };
 #pragma unroll
-    for (int p = 0; p < PD1; ++p)
+      for (int f = 0; f < FMR; ++f)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) wf[p][t] = frag(p, t);
-    uint4 w2q[PD2];
+        for (int t = 0; t < 4; ++t) nx[f][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      bf16x8 wf[PD1][4];
 #pragma unroll
-    for (int s = 0; s < KT; ++s) {
-      const int sl = s % PD1;
-      bf16x8 cw[4];
+      for (int p = 0; p < PD1; ++p)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) cw[t] = wf[sl][t];
-      if (s + PD1 < KT) {
+        for (int t = 0; t < 4; ++t) wf[p][t] = frag(p, t);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) wf[sl][t] = frag(s + PD1, t);
-      } else if (s + PD1 - KT < PD2) {
-        w2q[s + PD1 - KT] = w2[((s + PD1 - KT) * 16 + l16) * 4 + p2];
+      for (int s = 0; s < KT; ++s) {
+        const int sl = s % PD1;
+        bf16x8 cw[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) cw[t] = wf[sl][t];
+        if (s + PD1 < KT) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) wf[sl][t] = frag(s + PD1, t);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int f = 0; f < FMR; ++f) nx[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cw[t], ar[f][s], nx[f][t], 0, 0, 0);
+        if constexpr (GL) {  // two of the 16 GELUs (f, hh, r) per k-step
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int v = 2 * s + u;
+            if (v < 8 * FMR) gv[v >> 3][v & 7] = gelu_val(cu, cn - 1, v >> 3, (v >> 2) & 1, v & 3);
+          }
+        }
       }
+    };
+    auto gemm2 = [&](int c, bf16x8 (&gv)[FMR]) __attribute__((always_inline)) {
+      const uint4* w2 = lds + (c & 1) * STAGE + WIMG;
+      uint4 w2q[PD2];
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+      for (int q = 0; q < PD2; ++q) w2q[q] = w2[(q * 16 + l16) * 4 + p2];
 #pragma unroll
-        for (int f = 0; f < FMR; ++f) acc[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cw[t], ar[f][s], acc[f][t], 0, 0, 0);
-    }
+      for (int t = 0; t < NT2; ++t) {
+        const bf16x8 wv = __builtin_bit_cast(bf16x8, w2q[t % PD2]);
+        if (t + PD2 < NT2) w2q[t % PD2] = w2[((t + PD2) * 16 + l16) * 4 + p2];
 #pragma unroll
-    for (int q = PD1; q < PD2; ++q) w2q[q] = w2[(q * 16 + l16) * 4 + p2];
-    const float* bb = b1s + c * 64 + 4 * lg;
-    const float4 bh0 = *(const float4*)(bb), bg0 = *(const float4*)(bb + 16);
-    const float4 bh1 = *(const float4*)(bb + 32), bg1 = *(const float4*)(bb + 48);
-    const float hb0[4] = {bh0.x, bh0.y, bh0.z, bh0.w}, gb0[4] = {bg0.x, bg0.y, bg0.z, bg0.w};
-    const float hb1[4] = {bh1.x, bh1.y, bh1.z, bh1.w}, gb1[4] = {bg1.x, bg1.y, bg1.z, bg1.w};
+        for (int f = 0; f < FMR; ++f) out[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, gv[f], out[f][t], 0, 0, 0);
+      }
+    };
+    f32x4 accA[FMR][4], accB[FMR][4];
     bf16x8 gv[FMR];
+    bar();  // T(-1): W1(0), W2(0) landed; phase A's stages are free
+    issue_w1(1);
+    gemm1(0, accA, accB, gv, std::false_type{});
+    // iteration c: T(c) (W1(c + 1), W2(c) landed), issue W1(c + 2), W2(c + 1),
+    // GEMM1(c + 1) with GELU(c), GEMM2(c)
+    auto iter = [&](int c, f32x4 (&cu)[FMR][4], f32x4 (&nx)[FMR][4]) __attribute__((always_inline)) {
+      bar();
+      if (c + 2 < NCH) issue_w1(c + 2);
+      if (c + 1 < NCH) issue_w2(c + 1);
+      if (c + 1 < NCH) {
+        gemm1(c + 1, nx, cu, gv, std::true_type{});
+      } else {
 #pragma unroll
-    for (int f = 0; f < FMR; ++f)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        gv[f][r] = (__bf16)((acc[f][0][r] + hb0[r]) * gelu_erf(acc[f][1][r] + gb0[r]));
-        gv[f][4 + r] = (__bf16)((acc[f][2][r] + hb1[r]) * gelu_erf(acc[f][3][r] + gb1[r]));
+        for (int v = 0; v < 8 * FMR; ++v) gv[v >> 3][v & 7] = gelu_val(cu, c, v >> 3, (v >> 2) & 1, v & 3);
       }
-#pragma unroll
-    for (int t = 0; t < NT2; ++t) {
-      const bf16x8 wv = __builtin_bit_cast(bf16x8, w2q[t % PD2]);
-      if (t + PD2 < NT2) w2q[t % PD2] = w2[((t + PD2) * 16 + l16) * 4 + p2];
-#pragma unroll
-      for (int f = 0; f < FMR; ++f) out[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, gv[f], out[f][t], 0, 0, 0);
+      gemm2(c, gv);
+    };
+    static_assert(NCH % 2 == 0, "ff_chain: an even chunk count");
+    for (int c = 0; c < NCH; c += 2) {
+      iter(c, accA, accB);
+      iter(c + 1, accB, accA);
     }
+    // phase C's first stage into stage 0 once every wave is done with the FeedForward's slots
+    __syncthreads();
+    issue(NA + NCH, (NA + NCH) & 1);
+  } else {
+    for (int c = 0; c < NCH; ++c) {
+      const uint4* cur = top(NA + c);
+      f32x4 acc[FMR][4];
+  #pragma unroll
+      for (int f = 0; f < FMR; ++f)
+  #pragma unroll
+        for (int t = 0; t < 4; ++t) acc[f][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      auto frag = [&](int s, int t) {
+        return __builtin_bit_cast(bf16x8, cur[(s >> 1) * 512 + swz_bk<64>(t * 16 + l16, (s & 1) * 4 + lg)]);
+      };
+      const uint4* w2 = cur + WIMG;
+      bf16x8 wf[PD1][4];
+  #pragma unroll
+      for (int p = 0; p < PD1; ++p)
+  #pragma unroll
+        for (int t = 0; t < 4; ++t) wf[p][t] = frag(p, t);
+      uint4 w2q[PD2];
+  #pragma unroll
+      for (int s = 0; s < KT; ++s) {
+        const int sl = s % PD1;
+        bf16x8 cw[4];
+  #pragma unroll
+        for (int t = 0; t < 4; ++t) cw[t] = wf[sl][t];
+        if (s + PD1 < KT) {
+  #pragma unroll
+          for (int t = 0; t < 4; ++t) wf[sl][t] = frag(s + PD1, t);
+        } else if (s + PD1 - KT < PD2) {
+          w2q[s + PD1 - KT] = w2[((s + PD1 - KT) * 16 + l16) * 4 + p2];
+        }
+  #pragma unroll
+        for (int t = 0; t < 4; ++t)
+  #pragma unroll
+          for (int f = 0; f < FMR; ++f) acc[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cw[t], ar[f][s], acc[f][t], 0, 0, 0);
+      }
+  #pragma unroll
+      for (int q = PD1; q < PD2; ++q) w2q[q] = w2[(q * 16 + l16) * 4 + p2];
+      const float* bb = b1s + c * 64 + 4 * lg;
+      const float4 bh0 = *(const float4*)(bb), bg0 = *(const float4*)(bb + 16);
+      const float4 bh1 = *(const float4*)(bb + 32), bg1 = *(const float4*)(bb + 48);
+      const float hb0[4] = {bh0.x, bh0.y, bh0.z, bh0.w}, gb0[4] = {bg0.x, bg0.y, bg0.z, bg0.w};
+      const float hb1[4] = {bh1.x, bh1.y, bh1.z, bh1.w}, gb1[4] = {bg1.x, bg1.y, bg1.z, bg1.w};
+      bf16x8 gv[FMR];
+  #pragma unroll
+      for (int f = 0; f < FMR; ++f)
+  #pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          gv[f][r] = (__bf16)((acc[f][0][r] + hb0[r]) * gelu_erf(acc[f][1][r] + gb0[r]));
+          gv[f][4 + r] = (__bf16)((acc[f][2][r] + hb1[r]) * gelu_erf(acc[f][3][r] + gb1[r]));
+        }
+  #pragma unroll
+      for (int t = 0; t < NT2; ++t) {
+        const bf16x8 wv = __builtin_bit_cast(bf16x8, w2q[t % PD2]);
+        if (t + PD2 < NT2) w2q[t % PD2] = w2[((t + PD2) * 16 + l16) * 4 + p2];
+  #pragma unroll
+        for (int f = 0; f < FMR; ++f) out[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, gv[f], out[f][t], 0, 0, 0);
+      }
+    }
+
   }
 
   // ---- phase C: z = y Wp^T + bp + xb ----
