@@ -106,20 +106,32 @@ def test_process_request_through_gpu_worker(tmp_path, monkeypatch):
     vae = AutoencoderKL(block_out_channels=VAE_CH).init_weights(4)
     em, er, init = torch.from_numpy(inp["em"]), torch.from_numpy(inp["er"]), torch.from_numpy(inp["init"])
     mask = torch.from_numpy(inp["mask"])
+    from oracle.bf16_emul import bf16_storage, bf16_weights
+    to_u8 = lambda x: ((x / 2 + 0.5).clamp(0, 1) * 255).to(torch.uint8).permute(0, 2, 3, 1).numpy().astype(np.float64)
     for w in range(n // FR):
         sl = slice(w * FR, (w + 1) * FR)
-        ref = R.pipeline_window(unet.state_dict(), dict(unet.config), vae._sd, torch.from_numpy(inp["faces"][sl]),
-                                mask, torch.from_numpy(inp["chunks"][sl]), init[:, :, sl][:, :, :1], em[sl], er[sl],
-                                num_steps=int(inp["steps"]), guidance_scale=float(inp["guidance"]))
+        args = (torch.from_numpy(inp["faces"][sl]), mask, torch.from_numpy(inp["chunks"][sl]), init[:, :, sl][:, :, :1],
+                em[sl], er[sl])
+        kw = dict(num_steps=int(inp["steps"]), guidance_scale=float(inp["guidance"]))
+        ref = R.pipeline_window(unet.state_dict(), dict(unet.config), vae._sd, *args, **kw)
+        # the same window with bf16 storage emulated (bf16 weights, every op output rounded):
+        # the deviation bf16 storage alone produces (oracle/bf16_emul.py)
+        with bf16_storage():
+            emu = R.pipeline_window(bf16_weights(unet.state_dict()), dict(unet.config), bf16_weights(vae._sd), *args,
+                                    **kw)
         # the uint8 frames the pipeline writes: (x / 2 + 0.5).clamp(0, 1) * 255, truncated
-        ref_u8 = ((ref / 2 + 0.5).clamp(0, 1) * 255).to(torch.uint8).permute(0, 2, 3, 1).numpy().astype(np.float64)
+        ref_u8, emu_u8 = to_u8(ref), to_u8(emu)
         got = out[sl].astype(np.float64)
         e = rel_err(got / 255.0 * 2 - 1, torch.from_numpy(ref_u8 / 255.0 * 2 - 1))
-        d = np.abs(got - ref_u8)
-        print("served window", w, "rel", e, "max", d.max(), "p99.9", np.percentile(d, 99.9))
+        d, de = np.abs(got - ref_u8), np.abs(emu_u8 - ref_u8)
+        p, pe = np.percentile(d, 99.9), np.percentile(de, 99.9)
+        print(f"served window {w}: GPU vs fp32 oracle rel {e:.4f} max {d.max():.0f} p99.9 {p:.0f}; "
+              f"bf16-emulated oracle vs fp32 oracle max {de.max():.0f} p99.9 {pe:.0f}")
         # the window tolerance of tests/test_gpu_pipeline.py (tiny random-weight UNet, CFG 1.5,
-        # 2 steps: rel-L2 < 3e-2) plus per-pixel bounds on the like-for-like (truncated) uint8
-        # frames: max <= 12 levels, 99.9th percentile <= 6.  Measured on the box (r05b):
-        # rel 0.0155, max 9, p99.9 6.0 -- this tiny random-weight UNet amplifies bf16 error
-        # ~2x over the stage2 model, whose full-size windows hold p99.9 <= 3 (test_gpu_fullsize)
-        assert e < 3e-2 and d.max() <= 12 and np.percentile(d, 99.9) <= 6
+        # 2 steps: rel-L2 < 3e-2) and per-pixel bounds on the like-for-like (truncated) uint8
+        # frames, measured against what bf16 storage alone produces on the same window: the
+        # GPU's p99.9 within 2 levels and its max within 4 levels of the emulation's, and
+        # p99.9 <= 6 / max <= 12 outright (on this tiny random-weight model the
+        # emulation itself reaches max 8, p99.9 4-5 in the mouth region)
+        assert e < 3e-2 and d.max() <= 12 and p <= 6
+        assert p <= pe + 2 and d.max() <= de.max() + 4
