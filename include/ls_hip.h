@@ -425,7 +425,8 @@ int ls_add_rows(const uint16_t* x, int64_t rows, int32_t C, int32_t ldx, const f
  * 13, 14 are measured-slower A/B options; key 15 = K = 640 row-block GEMM with two
  * 16-row fragments per wave (256-row blocks; default on); key 16 = 128-column halo tiles on 16 x 8
  * patches, two blocks per CU, for Cin <= 256 (default on; off: 16 x 16, one block per CU);
- * key 17 = ls_ff_chain rows per wave: 2 = 32 rows, one wave per SIMD (default), 1 = 16 rows. */
+ * key 17 = ls_ff_chain rows per wave: 1 = 16 rows (default), 2 = 32 rows, one wave per SIMD
+ * (measured slower; diagnostics build only). */
 int ls_set_tuning(int32_t key, int32_t value);
 
 /* Diagnostics: workgroups per CU the runtime can co-schedule for a GEMM kernel

@@ -833,8 +833,11 @@ __global__ void __launch_bounds__(512, 1) ff_pair_kernel(FFArgs a) {
 
 using namespace ls;
 
-// rows per wave of ls_ff_chain: 32 (2, the default) or 16 (1) -- ls_set_tuning key 17
-int g_ff_chain_fmr = 2;
+// rows per wave of ls_ff_chain: 16 (1, the default) or, in the diagnostics build, 32 (2) --
+// ls_set_tuning key 17.  Measured and rejected (profiles/r06c_kernel.txt, same box, M = 786432):
+// 32 rows, one wave per SIMD 3058 us straight / 5120 us software-pipelined (AGPR traffic and
+// scratch in the chunk loop) against 2695 us at 16 rows
+int g_ff_chain_fmr = 1;
 
 extern "C" int ls_ff_chain(const ls_ff_chain_desc* d, void* stream) {
   if (!d || !d->o || !d->wo || !d->bo || !d->h1 || !d->w1 || !d->b1 || !d->w2 || !d->b2 || !d->wp || !d->bp ||
@@ -857,13 +860,15 @@ extern "C" int ls_ff_chain(const ls_ff_chain_desc* d, void* stream) {
   a.M = d->M; a.ldo = d->ldo; a.ldh = d->ldh; a.ldxb = d->ldxb; a.ldz = d->ldz; a.eps = d->eps;
   constexpr int C = 320, I = 1280;
   const size_t shm = (size_t)2 * (64 * (C / 64) * 8 + C * 4) * 16 + 2 * I * sizeof(float);
-  if (g_ff_chain_fmr == 1) {
-    LS_SET_MAX_DYN_SHM((ff_chain_kernel<C, I, 1>), (int)shm);
-    ff_chain_kernel<C, I, 1><<<(unsigned)(d->M / 128), 512, shm, (hipStream_t)stream>>>(a);
-  } else {
+#ifdef LS_DIAG_KERNELS
+  if (g_ff_chain_fmr == 2) {
     LS_SET_MAX_DYN_SHM((ff_chain_kernel<C, I, 2>), (int)shm);
     ff_chain_kernel<C, I, 2><<<(unsigned)(d->M / 128), 256, shm, (hipStream_t)stream>>>(a);
+    return check_launch("ff_chain_kernel");
   }
+#endif
+  LS_SET_MAX_DYN_SHM((ff_chain_kernel<C, I, 1>), (int)shm);
+  ff_chain_kernel<C, I, 1><<<(unsigned)(d->M / 128), 512, shm, (hipStream_t)stream>>>(a);
   return check_launch("ff_chain_kernel");
 }
 

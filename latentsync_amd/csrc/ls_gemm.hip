@@ -2975,6 +2975,9 @@ extern int g_ff_chain_fmr;  // ls_ff.hip
 extern "C" int ls_set_tuning(int32_t key, int32_t value) {
   switch (key) {
     case 17:
+#ifndef LS_DIAG_KERNELS
+      if (value == 2) return fail(LS_ERR_INVALID, "ls_ff_chain at 32 rows per wave: diagnostics build only");
+#endif
       if (value != 1 && value != 2) return fail(LS_ERR_INVALID, "ls_ff_chain rows per wave: 1 (16) or 2 (32)");
       g_ff_chain_fmr = value;
       return LS_OK;

@@ -51,11 +51,12 @@ def timed(fn, n=10):
 
 
 fl = 4.0 * M * C * C + 6.0 * M * C * I
-for fmr in (2, 1):
-    lib.ls_set_tuning(17, fmr)
+for fmr in (1, 2):
+    if lib.ls_set_tuning(17, fmr) != 0:
+        continue  # 32 rows per wave: diagnostics build only
     t = timed(lambda: ops.ff_chain(o, h1, xb, chain))
     print(f"ls_ff_chain M={M} rows/wave {16 * fmr}: {t:.1f} us, {fl / t / 1e6:.1f} TF/s")
-lib.ls_set_tuning(17, 2)
+lib.ls_set_tuning(17, 1)
 t = timed(unfused)
 print(f"unfused (to_out + ls_feedforward + proj_out) M={M}: {t:.1f} us, {fl / t / 1e6:.1f} TF/s")
 t = timed(lambda: ops.feedforward(h1, st, ff1, ff2, ff2p))

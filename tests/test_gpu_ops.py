@@ -691,7 +691,7 @@ def test_rowblock640_affine_odd_sample_rows(gpu, fm2):
     assert rel_err(y, y_tiled) < 1e-2
 
 
-@pytest.mark.parametrize("fmr", [2, 1])
+@pytest.mark.parametrize("fmr", [1, 2])
 @pytest.mark.parametrize("M", [128 * 3, 65536, 786432])
 def test_ff_chain(gpu, M, fmr):
     """ls_ff_chain: h2 = o Wo^T + bo + h1, z = (h2 + FF(LN(h2))) Wp^T + bp + xb in one launch
@@ -721,11 +721,12 @@ def test_ff_chain(gpu, M, fmr):
     assert ops.ff_chain_ok(od, chain)
     from latentsync_amd import _lib
     lib = _lib.load()
-    assert lib.ls_set_tuning(17, fmr) == 0  # rows per wave: 32 (default) / 16
+    if lib.ls_set_tuning(17, fmr) != 0:  # rows per wave: 16 (default) / 32 (diagnostics build)
+        pytest.skip("32 rows per wave: diagnostics build only")
     try:
         z = ops.ff_chain(od, h1d, xbd, chain)
     finally:
-        lib.ls_set_tuning(17, 2)
+        lib.ls_set_tuning(17, 1)
     cs = z.gn_cs
     # unfused GPU path
     st = torch.empty((M, 2), dtype=torch.float32, device=DEV)
