@@ -48,7 +48,7 @@ def _deps():
 # tests/test_build_guards.py checks that every kernel with a non-zero counted wait in csrc/ is listed.
 COUNTED_VMCNT = ("gemm_rowblock_kernel", "conv_gemm_dma_kernel", "attn5_kernel", "attn8_kernel", "tattn_fused_kernel",
                  "attnw_kernel", "conv3x3_halo_kernel", "attn6_kernel", "conv_gemm_p8_kernel", "conv_gemm_big4_kernel",
-                 "conv_gemm_areg_kernel", "ff_pair_kernel")
+                 "conv_gemm_areg_kernel", "ff_pair_kernel", "ff_chain_kernel")
 
 
 def _spills(stderr):
