@@ -250,21 +250,19 @@ __global__ void __launch_bounds__(512 / FMR, 1) ff_chain_kernel(FFChainArgs a) {
   constexpr int WIMG = 64 * (C / 64) * 8; // uint4: W1 chunk
   constexpr int W2IMG = C * 4;            // uint4: one [C][32] k-step image (W2 chunk, Wo / Wp k-step)
   constexpr int STAGE = WIMG + W2IMG;
-  constexpr int NSL = 2 * STAGE / W2IMG;  // k-step image slots of the projection ring (phases A / C)
-  constexpr int AHEAD = NSL - 1;          // images in flight ahead of the one computed
+  constexpr int KPS = STAGE / W2IMG;      // k-step images per stage in phases A / C
+  constexpr int NA = (KT + KPS - 1) / KPS;  // stages of phase A (and of phase C)
   constexpr int NT2 = C / 16;             // output tiles
   constexpr int PW1 = WIMG / NT;
   constexpr int UW2 = W2IMG / 64;
-  constexpr int IWI = (UW2 + NW - 1) / NW;  // DMA wave-instructions per wave and image (padded: uniform)
   constexpr int PD1 = 2, PD2 = 6;
   constexpr int ZP = C + 8;               // LDS pitch (bf16) of the block's result image
   constexpr int RG = NT >= C ? 4 : 2;     // row groups of the column-sum pass
-  static_assert(STAGE % W2IMG == 0 && AHEAD >= 2 && KT > AHEAD && WIMG % NT == 0, "ff_chain stage layout");
+  static_assert(STAGE % W2IMG == 0 && KPS >= 1 && WIMG % NT == 0, "ff_chain stage layout");
   static_assert(2 * STAGE * 16 >= 128 * ZP * 2 + RG * (C / 4) * 8 * 4, "ff_chain epilogue LDS");
   static_assert(C == 320 && I == 1280 && (FMR == 1 || FMR == 2), "ff_chain shape");
-  extern __shared__ __attribute__((aligned(16))) uint4 lds[];  // [2][STAGE], b1 (2I fp32), 1 KB dummy
+  extern __shared__ __attribute__((aligned(16))) uint4 lds[];  // [2][STAGE], then b1 (2I fp32)
   float* b1s = (float*)(lds + 2 * STAGE);
-  uint4* const dummy = lds + 2 * STAGE + 2 * I / 4;  // landing slot of the padding DMAs
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, lg = lane >> 4;
@@ -273,50 +271,34 @@ __global__ void __launch_bounds__(512 / FMR, 1) ff_chain_kernel(FFChainArgs a) {
 
   for (int i = tid; i < 2 * I / 4; i += NT) ((float4*)b1s)[i] = ((const float4*)a.b1)[i];
 
-  // Phases A / C (Wo, Wp): k-step image j ([C][32], 20 KB) in ring slot j % NSL of the two
-  // stages' LDS, AHEAD images in flight (a ring of whole 3-image stages, one stage ahead, had
-  // every stage wait out its DMA).  Every wave issues IWI DMAs per image (padding ones land in
-  // `dummy`), so "image j landed" is one constant vmcnt.  FeedForward chunk c (W1 + W2) sits
-  // in stage c & 1.
-  auto issue_img = [&](const u16* w, int j) __attribute__((always_inline)) {
-    uint4* dst = lds + (j % NSL) * W2IMG;
-    // the lane's source offset recomputed per call (laundered): kept live across the
-    // FeedForward loop for phase C's images, the addresses spilled
-    int ln = lane * 8;
-    asm volatile("" : "+v"(ln));
-    const u16* src = w + (long)j * W2IMG * 8 + ln;
+  // chunk g of the launch: [0, NA) Wo stages, [NA, NA + NCH) FeedForward chunks, then Wp stages
+  auto issue = [&](int g, int st) __attribute__((always_inline)) {
+    uint4* dst = lds + st * STAGE;
+    if (g < NA || g >= NA + NCH) {
+      const int q = g < NA ? g : g - NA - NCH;
+      const int nk = min(KPS, KT - q * KPS);
+      const u16* src = (g < NA ? a.wo : a.wp) + (long)q * KPS * W2IMG * 8;
+      for (int u = wid; u < nk * UW2; u += NW) glds16(src + ((long)u * 64 + lane) * 8, dst + u * 64);
+    } else {
+      const int c = g - NA;
 #pragma unroll
-    for (int i = 0; i < IWI; ++i) {
-      const int u = wid + i * NW;  // wave-uniform
-      glds16(src + (long)(u < UW2 ? u : 0) * 64 * 8, u < UW2 ? dst + u * 64 : dummy);
+      for (int p = 0; p < PW1; ++p) {  // piece q: image q >> 9, row (q >> 3) & 63, physical chunk q & 7
+        const int q = p * NT + tid, r = (q >> 3) & 63, pc = q & 7;
+        const int lc = pc ^ ((r >> 1) & 7);
+        glds16(a.w1 + (long)(c * 64 + r) * C + (q >> 9) * 64 + lc * 8, dst + p * NT + wid * 64);
+      }
+      for (int u = wid; u < UW2; u += NW) glds16(a.w2 + ((long)c * W2IMG + u * 64 + lane) * 8, dst + WIMG + u * 64);
     }
   };
-  auto issue_ff = [&](int c) __attribute__((always_inline)) {
-    uint4* dst = lds + (c & 1) * STAGE;
-#pragma unroll
-    for (int p = 0; p < PW1; ++p) {  // piece q: image q >> 9, row (q >> 3) & 63, physical chunk q & 7
-      const int q = p * NT + tid, r = (q >> 3) & 63, pc = q & 7;
-      const int lc = pc ^ ((r >> 1) & 7);
-      glds16(a.w1 + (long)(c * 64 + r) * C + (q >> 9) * 64 + lc * 8, dst + p * NT + wid * 64);
-    }
-    for (int u = wid; u < UW2; u += NW) glds16(a.w2 + ((long)c * W2IMG + u * 64 + lane) * 8, dst + WIMG + u * 64);
-  };
-  auto sync = [&]() __attribute__((always_inline)) {
+  auto top = [&](int g) __attribute__((always_inline)) {  // chunk g's DMA landed everywhere; refill the other stage
+    wait_vm<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if (g + 1 < 2 * NA + NCH) issue(g + 1, (g + 1) & 1);
+    return (const uint4*)(lds + (g & 1) * STAGE);
   };
-  auto top = [&](int c) __attribute__((always_inline)) {  // FeedForward chunk c landed everywhere
-    wait_vm<0>();
-    sync();
-    if (c + 1 < NCH) {
-      issue_ff(c + 1);
-    } else {  // the other stage is free: phase C's first images
-#pragma unroll
-      for (int j = 0; j < NSL / 2; ++j) issue_img(a.wp, j);
-    }
-    return (const uint4*)(lds + (c & 1) * STAGE);
-  };
+  issue(0, 0);
 
   const int p2 = lg ^ (((l16 >> 3) & 1) << 1);  // this lane's physical piece of a [C][32] image
   bf16x8 ar[FMR][KT];   // the B operand of the current phase: o rows, LN(h2), y
@@ -329,38 +311,41 @@ __global__ void __launch_bounds__(512 / FMR, 1) ff_chain_kernel(FFChainArgs a) {
       for (int f = 0; f < FMR; ++f) out[f][t] = (f32x4){b.x, b.y, b.z, b.w};
     }
   };
-  // GEMM0 / GEMM3 over the KT k-step images of a [C][C] weight (images 0 .. AHEAD - 1 already
-  // issued), operand ar; after the last image's barrier `next` issues what follows the phase
-  auto proj = [&](const u16* w, auto next) __attribute__((always_inline)) {
+  // GEMM0 / GEMM3 over the NA stages of a [C][C] weight, operand ar (compile-time k-steps)
+  auto proj = [&](int g0) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < KT; ++j) {
-      // image j landed: younger DMAs are images j + 1 .. min(j + AHEAD - 1, KT - 1), IWI each
-      if (KT - 1 - j >= AHEAD - 1) wait_vm<IWI * (AHEAD - 1)>();
-      else if (KT - 1 - j == 3) wait_vm<IWI * 3>();
-      else if (KT - 1 - j == 2) wait_vm<IWI * 2>();
-      else if (KT - 1 - j == 1) wait_vm<IWI>();
-      else wait_vm<0>();
-      sync();
-      if (j + AHEAD < KT) issue_img(w, j + AHEAD);  // into the slot image j - 1 left
-      else if (j == KT - 1) next();
-      // the image's lane offset, laundered so that the two projections' (same-valued) LDS
-      // addresses are not kept live across the FeedForward loop (they spilled there); a
-      // tile's offset within the image is an instruction immediate
-      int lo = (j % NSL) * W2IMG + l16 * 4 + p2;
-      asm volatile("" : "+v"(lo));
-      const uint4* cur = lds + lo;
+    for (int q = 0; q < NA; ++q) {
+      const uint4* cur = top(g0 + q);
+      const int nk = (q + 1) * KPS <= KT ? KPS : KT - q * KPS;
+      // per-image lane offsets, laundered so that the two projections' (same-valued) LDS
+      // addresses are not shared across the FeedForward loop (kept live there, they spilled);
+      // a tile's offset within an image is an instruction immediate
+      int lo[KPS];
+#pragma unroll
+      for (int j = 0; j < KPS; ++j) {
+        lo[j] = j * W2IMG + l16 * 4 + p2;
+        asm volatile("" : "+v"(lo[j]));
+      }
       uint4 wq[PD2];
 #pragma unroll
-      for (int i = 0; i < PD2; ++i) wq[i] = cur[i * 64];
+      for (int i = 0; i < PD2; ++i) wq[i] = cur[lo[i / NT2] + (i % NT2) * 64];
 #pragma unroll
-      for (int t = 0; t < NT2; ++t) {
-        const bf16x8 wv = __builtin_bit_cast(bf16x8, wq[t % PD2]);
-        if (t + PD2 < NT2) wq[t % PD2] = cur[(t + PD2) * 64];
+      for (int j = 0; j < KPS; ++j) {
+        if (j < nk) {
+          const int k = q * KPS + j < KT ? q * KPS + j : 0;
 #pragma unroll
-        for (int f = 0; f < FMR; ++f)
-          out[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, ar[f][j], out[f][t], 0, 0, 0);
+          for (int t = 0; t < NT2; ++t) {
+            const int i = j * NT2 + t;
+            const bf16x8 wv = __builtin_bit_cast(bf16x8, wq[i % PD2]);
+            const int n = i + PD2;
+            if (n < nk * NT2) wq[i % PD2] = cur[lo[n / NT2 < KPS ? n / NT2 : 0] + (n % NT2) * 64];
+#pragma unroll
+            for (int f = 0; f < FMR; ++f)
+              out[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, ar[f][k], out[f][t], 0, 0, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);  // one k-step at a time: hoisted fragment reads spill
+        }
       }
-      __builtin_amdgcn_sched_barrier(0);  // one k-step at a time: hoisted fragment reads spill
     }
   };
   // accumulators (bf16-rounded values) -> the operand registers in accumulator k order
@@ -376,15 +361,13 @@ __global__ void __launch_bounds__(512 / FMR, 1) ff_chain_kernel(FFChainArgs a) {
 
   // ---- phase A: h2 = o Wo^T + bo + h1 ----
 #pragma unroll
-  for (int f = 0; f < FMR; ++f) {  // the operand rows first: older than the images in the vmcnt order
+  for (int f = 0; f < FMR; ++f) {
     const u16* src = a.o + (row0 + wr0 + 16 * f) * a.ldo + lg * 8;
 #pragma unroll
     for (int s = 0; s < KT; ++s) ar[f][s] = *(const bf16x8*)(src + s * 32);
   }
-#pragma unroll
-  for (int j = 0; j < AHEAD; ++j) issue_img(a.wo, j);
   init_cols(a.bo);
-  proj(a.wo, [&]() { issue_ff(0); });  // after the last image: FeedForward chunk 0 into stage 0
+  proj(0);
 #pragma unroll
   for (int f = 0; f < FMR; ++f) {
     uint2 xr[NT2];
@@ -531,13 +514,12 @@ __global__ void __launch_bounds__(512 / FMR, 1) ff_chain_kernel(FFChainArgs a) {
       iter(c, accA, accB);
       iter(c + 1, accB, accA);
     }
-    // phase C's first images once every wave is done with the FeedForward's slots
+    // phase C's first stage into stage 0 once every wave is done with the FeedForward's slots
     __syncthreads();
-#pragma unroll
-    for (int j = 0; j < AHEAD; ++j) issue_img(a.wp, j);
+    issue(NA + NCH, (NA + NCH) & 1);
   } else {
     for (int c = 0; c < NCH; ++c) {
-      const uint4* cur = top(c);
+      const uint4* cur = top(NA + c);
       f32x4 acc[FMR][4];
   #pragma unroll
       for (int f = 0; f < FMR; ++f)
@@ -596,17 +578,11 @@ __global__ void __launch_bounds__(512 / FMR, 1) ff_chain_kernel(FFChainArgs a) {
 
   }
 
-  if constexpr (FMR == 1) {  // images 0 .. NSL/2 - 1 were issued at the last chunk's top
-    __syncthreads();           // every wave is done with the last chunk's stage
-#pragma unroll
-    for (int j = NSL / 2; j < AHEAD; ++j) issue_img(a.wp, j);
-  }
-
   // ---- phase C: z = y Wp^T + bp + xb ----
 #pragma unroll
   for (int f = 0; f < FMR; ++f) acc_to_operand(f, 0.f, 1.f);  // y, rounded to bf16 as the unfused path stores it
   init_cols(a.bp);
-  proj(a.wp, [&]() {});
+  proj(NA + NCH);
 
   // ---- epilogue: + xb, the block's 128 x C result through LDS: row stores + column sums ----
   __syncthreads();  // every wave is past its last stage reads
@@ -883,7 +859,7 @@ extern "C" int ls_ff_chain(const ls_ff_chain_desc* d, void* stream) {
   a.wp = (const u16*)d->wp; a.bp = d->bp; a.xb = (const u16*)d->xb; a.z = (u16*)d->z; a.cs_out = d->cs_out;
   a.M = d->M; a.ldo = d->ldo; a.ldh = d->ldh; a.ldxb = d->ldxb; a.ldz = d->ldz; a.eps = d->eps;
   constexpr int C = 320, I = 1280;
-  const size_t shm = (size_t)2 * (64 * (C / 64) * 8 + C * 4) * 16 + 2 * I * sizeof(float) + 1024;
+  const size_t shm = (size_t)2 * (64 * (C / 64) * 8 + C * 4) * 16 + 2 * I * sizeof(float);
 #ifdef LS_DIAG_KERNELS
   if (g_ff_chain_fmr == 2) {
     LS_SET_MAX_DYN_SHM((ff_chain_kernel<C, I, 2>), (int)shm);
