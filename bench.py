@@ -1,7 +1,7 @@
 """Benchmark: lip-synced frames/sec at 256x256, 16-frame window, 20 DDIM steps
 (BASELINE.json "metric", configs[1]; configs[3] when launched on N GPUs).
 
-One "step" = one batch of `--windows-per-batch` (default 32 at configs[1]) independent
+One "step" = one batch of `--windows-per-batch` (default 48 at configs[1]) independent
 16-frame windows of a clip through the whole hot path on one GPU: pixel prep ->
 VAE encode x2 -> 20 x (UNet3D fwd + CFG + DDIM) -> VAE decode -> paste-back,
 inputs resident in HBM.  Every window is computed exactly as alone (per-window
