@@ -54,27 +54,31 @@ def main():
     from fastapi.testclient import TestClient
 
     from latentsync_amd import serve as S
+    from latentsync_amd.pipeline import plan_window_batches
     d = tempfile.mkdtemp(prefix="ls_serve_")
     _clip(d, "c10", 160, 6.4)
     _clip(d, "c11", 176, 7.04)
+    # the audio of a clip of 16 w frames pads to w + 1 windows (repeat.pad_whisper_chunks_end)
     for w in (9, 25, 49):
-        _clip(d, f"c{w}", 16 * w, 16 * w / 25)
+        _clip(d, f"c{w}", 16 * (w - 1), 16 * (w - 1) / 25)
     worker = S.ProcessWorker(0, "serve_latency:random_stage2_pipeline", request_timeout=900.0, data_dir=d,
                              results_dir=os.path.join(d, "res"), resolution=256)
     app = S.create_app([worker])
     with TestClient(app) as c:
         for rid, vid, what in (("r1", "c10", "cold (engine build + capture)"),
                                ("r2", "c10", "warm"), ("r3", "c11", "a longer clip, same engine bucket"),
-                               ("r4", "c9", "exact-size engine, cold"), ("r5", "c25", "28-window engine, cold"),
-                               ("r6", "c25", "warm"), ("r7", "c49", "2 x 28 windows, same engine")):
+                               ("r4", "c9", "cold (bucket 12 would pad 33 %: exact size)"), ("r5", "c25", "cold"),
+                               ("r6", "c25", "warm"), ("r7", "c49", "the same engine")):
             t0 = time.time()
             r = c.post("/process", json={"id": rid, "video_id": vid, "audio_url": "file://" + os.path.join(d, f"{vid}.wav")})
             wall = time.time() - t0
             assert r.status_code == 200, r.text
             body = r.json()
             n = np.load(body["output_url"])["frames"].shape[0]
-            print(f"/process {n // 16} windows, {what}: {n} frames, server elapsed {body['elapsed_time']:.2f} s, client wall {wall:.2f} s, "
-                  f"{n / body['elapsed_time']:.1f} frames/s", flush=True)
+            E, batches = plan_window_batches(list(range(n // 16)), 48)
+            print(f"/process {n // 16} windows ({len(batches)} x {E}-window engine), {what}: {n} frames, server elapsed "
+                  f"{body['elapsed_time']:.2f} s, client wall {wall:.2f} s, {n / body['elapsed_time']:.1f} frames/s",
+                  flush=True)
 
 
 if __name__ == "__main__":
