@@ -119,7 +119,8 @@ int ls_conv2d(const ls_conv_desc* d, void* stream);
  * GEMM (K = 320 / 640 linears; also takes the GroupNorm affine prologue on its
  * register-resident A rows), 2 = register-staged tiled GEMM (affine prologue
  * elsewhere -- callers materialise the affine with ls_groupnorm_apply instead),
- * 3 = halo-tile 3x3 conv (ABI 12: 3x3 / stride 1 / pad 1, Cin % 64 == 0, W in {16, 32,
+ * 3 = halo-tile 3x3 conv (ABI 12: 3x3 / stride 1 / pad 1 (or a nearest-x2 upsample without an
+ * input affine, round 6), Cin % 64 == 0, W in {16, 32,
  * 64} or a multiple of 64, N % 160 or % 128 == 0; takes the GroupNorm affine + SiLU on
  * its input, once per pixel, and the dual-source concat), -1 = invalid descriptor.
  * Host-only, no launch. */
@@ -426,7 +427,8 @@ int ls_add_rows(const uint16_t* x, int64_t rows, int32_t C, int32_t ldx, const f
  * 16-row fragments per wave (256-row blocks; default on); key 16 = 128-column halo tiles on 16 x 8
  * patches, two blocks per CU, for Cin <= 256 (default on; off: 16 x 16, one block per CU);
  * key 17 = ls_ff_chain rows per wave: 1 = 16 rows (default), 2 = 32 rows, one wave per SIMD
- * (measured slower; diagnostics build only). */
+ * (measured slower; diagnostics build only); key 18 = nearest-x2 upsample convs on the halo-tile
+ * kernel (default on; off: the tiled gather). */
 int ls_set_tuning(int32_t key, int32_t value);
 
 /* Diagnostics: workgroups per CU the runtime can co-schedule for a GEMM kernel

@@ -2286,7 +2286,12 @@ __global__ void __launch_bounds__(TH_ / 4 * 128, 16 / TH_) conv3x3_halo_kernel(C
   const int tyb = bid % tpc;
   const int img = bid / tpc;
   const int y0 = tyb * TH, x0 = txb * TW, n0 = tn * BN;
-  const long HW = (long)a.H * a.W;
+  const long HW = (long)a.H * a.W;  // the OUTPUT image (for an upsample conv the launch passes the output dims)
+  // nearest x2 upsample (round 6): halo pixel (y, x) of the output image reads input pixel
+  // (y >> 1, x >> 1) -- the LDS halo image, the taps and the epilogue are those of a plain conv
+  const int ups = a.upsample;
+  const int Wi = a.W >> ups;
+  const long HWi = HW >> (2 * ups);
   const int nchunk = a.Cin / 64;
   const int G = 9 * nchunk;  // taps in all
 
@@ -2308,11 +2313,11 @@ __global__ void __launch_bounds__(TH_ / 4 * 128, 16 / TH_) conv3x3_halo_kernel(C
       const int slot = hr * P + hcol + 3;
       hdst[j] = slot * 8 + (hc8 ^ (slot & 7));
     }
-    hpix[j] = q < NPC && y >= 0 && y < a.H && x >= 0 && x < a.W ? y * a.W + x : -1;
+    hpix[j] = q < NPC && y >= 0 && y < a.H && x >= 0 && x < a.W ? (y >> ups) * Wi + (x >> ups) : -1;
   }
   const uint32_t cap = 0x7FFFFFFFu;
-  const i32x4 rs1 = buffer_rsrc(a.x1 + img * HW * a.ld1, (uint32_t)min((long)HW * a.ld1 * 2, (long)cap));
-  const i32x4 rs2 = a.C2 ? buffer_rsrc(a.x2 + img * HW * a.ld2, (uint32_t)min((long)HW * a.ld2 * 2, (long)cap)) : rs1;
+  const i32x4 rs1 = buffer_rsrc(a.x1 + img * HWi * a.ld1, (uint32_t)min((long)HWi * a.ld1 * 2, (long)cap));
+  const i32x4 rs2 = a.C2 ? buffer_rsrc(a.x2 + img * HWi * a.ld2, (uint32_t)min((long)HWi * a.ld2 * 2, (long)cap)) : rs1;
   const long aff0 = (long)img * HW / a.pix_per_sample * a.Cin;
   uint4 hreg[HB];
   float4 gp;
@@ -2819,15 +2824,21 @@ static void launch_cfg(const ConvArgs& a, int ks, bool tapu, int grid, hipStream
 
 // ---- halo-tile 3x3 conv dispatch (conv3x3_halo_kernel)
 static bool g_halo = ls_env("LS_HALO") == nullptr || atoi(ls_env("LS_HALO")) != 0;  // A/B switch: LS_HALO=0
+// the nearest-x2 upsample convs on the halo kernel too (tuning key 18; off: the tiled gather)
+static bool g_halo_ups = ls_env("LS_HALO_UPS") == nullptr || atoi(ls_env("LS_HALO_UPS")) != 0;
 // A/B switch (tuning key 13): 128-channel tiles where both divide N (3-slot weight ring
 // instead of 2 at BN 160)
 static bool g_halo_bn128 = ls_env("LS_HALO_BN128") != nullptr;
 
 // patch width of the halo conv for this call (0: not taken)
 static int halo_tw(const ls_conv_desc* d, const ConvArgs& a) {
-  if (!g_halo || g_force_tile || g_force_regstage || d->ksize != 3 || a.stride != 1 || a.pad != 1 || a.upsample ||
+  if (!g_halo || g_force_tile || g_force_regstage || d->ksize != 3 || a.stride != 1 || a.pad != 1 ||
       !a.ccm || a.Cin % 64 || a.C1 % 64 || a.K != 9 * a.Cin || a.y_f32 || a.act != LS_ACT_NONE ||
-      a.ln_mr || a.stats_out || a.ldy % 8 || (a.res && a.ldr % 8) || a.Ho != a.H || a.Wo != a.W)
+      a.ln_mr || a.stats_out || a.ldy % 8 || (a.res && a.ldr % 8))
+    return 0;
+  // nearest x2 upsample (Upsample3D, resnet.py:53-71; round 6): no input affine (the UNet's
+  // upsampler conv has none); the halo image is built in output space from the input pixels
+  if (a.upsample ? (!g_halo_ups || a.aff_scale || a.Ho != 2 * a.H || a.Wo != 2 * a.W) : (a.Ho != a.H || a.Wo != a.W))
     return 0;
   // N <= 640: with more output channels the patch is re-loaded and re-transformed per N tile
   // and the tiled 256x256 kernel wins (VAE 512 channels at 32^2: 3667 vs 3409 us; 128 at
@@ -2838,7 +2849,7 @@ static int halo_tw(const ls_conv_desc* d, const ConvArgs& a) {
   if (((uintptr_t)a.x1 | (uintptr_t)a.x2 | (uintptr_t)a.w) & 15 || a.ld1 % 8 || (a.C2 && a.ld2 % 8)) return 0;
   // 16 x 16 patches everywhere: the smallest halo overhead ((16 + 2)^2 / 256 = 1.27 input
   // pixels per output pixel; 32 x 8: 1.33, 64 x 4: 1.55) and no register spills
-  const int tw = (a.W % 16 == 0 && a.H % 16 == 0) ? 16 : 0;
+  const int tw = (a.Wo % 16 == 0 && a.Ho % 16 == 0) ? 16 : 0;
   if (!tw) return 0;
   if ((long)a.H * a.W * a.ld1 * 2 >= (1L << 31) || (a.C2 && (long)a.H * a.W * a.ld2 * 2 >= (1L << 31)))
     return 0;  // per-image buffer descriptors
@@ -2880,6 +2891,13 @@ static void launch_halo1(const ConvArgs& a, hipStream_t s) {
 
 static void launch_halo(const ConvArgs& a, int tw, hipStream_t s) {
   (void)tw;  // (16: the only patch width compiled)
+  if (a.upsample) {  // the kernel works in output space: H, W = the output image
+    ConvArgs o = a;
+    o.H = a.Ho;
+    o.W = a.Wo;
+    launch_halo1<16>(o, s);
+    return;
+  }
   launch_halo1<16>(a, s);
 }
 
@@ -2974,6 +2992,7 @@ extern int g_ff_chain_fmr;  // ls_ff.hip
 
 extern "C" int ls_set_tuning(int32_t key, int32_t value) {
   switch (key) {
+    case 18: g_halo_ups = value != 0; return LS_OK;
     case 17:
 #ifndef LS_DIAG_KERNELS
       if (value == 2) return fail(LS_ERR_INVALID, "ls_ff_chain at 32 rows per wave: diagnostics build only");

@@ -114,3 +114,43 @@ def test_halo_conv_path_code(gpu):
     x8 = torch.zeros(2, 8, 8, 128, dtype=torch.bfloat16, device=DEV)
     assert ops.conv_path(x8, pw) != 3
     assert ops.conv_path(x, pw, stride=2, pad=1) != 3
+
+
+@pytest.mark.parametrize("n,H,W,Cin,N,res", [
+    (4, 16, 16, 640, 640, False),     # the UNet's 16x16 -> 32x32 upsampler conv (up_blocks.1)
+    (2, 8, 16, 128, 256, True),       # 128-column tiles (16 x 8 patches), residual, non-square
+    (2, 32, 32, 256, 256, False),     # a VAE-like upsampler conv
+])
+def test_halo_conv_upsample(gpu, n, H, W, Cin, N, res):
+    """Nearest-x2 upsample + 3x3 conv (Upsample3D, resnet.py:53-71) on the halo kernel (tuning
+    key 18): halo pixel (y, x) of the output reads input pixel (y >> 1, x >> 1).  Against fp32
+    (F.interpolate nearest + F.conv2d) and the tiled gather path, with the GroupNorm column sums."""
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(n * 100 + H + Cin + N)
+    x = _bf(torch.randn(n, H, W, Cin, generator=g))
+    w = torch.randn(N, Cin, 3, 3, generator=g) / (9 * Cin) ** 0.5
+    b = 0.1 * torch.randn(N, generator=g)
+    rv = _bf(torch.randn(n, 2 * H, 2 * W, N, generator=g)) if res else None
+    pw = ops.Packed(pack_weight(w).to(torch.bfloat16).to(DEV), b.to(DEV), Cin, 3, N)
+    xd = x.to(torch.bfloat16).to(DEV)
+    kw = dict(upsample=True)
+    if res:
+        kw["res"] = rv.to(torch.bfloat16).to(DEV)
+    assert ops.conv_path(xd, pw, **kw) == 3
+    y = ops.conv(xd, pw, gn_out=True, **kw)
+    cs = y.gn_cs.clone()
+    assert lib.ls_set_tuning(18, 0) == 0
+    try:
+        assert ops.conv_path(xd, pw, **kw) != 3
+        y2 = ops.conv(xd, pw, gn_out=True, **kw)
+    finally:
+        lib.ls_set_tuning(18, 1)
+    up = F.interpolate(x.permute(0, 3, 1, 2), scale_factor=2.0, mode="nearest")
+    ref = F.conv2d(up, w, b, padding=1).permute(0, 2, 3, 1)
+    if res:
+        ref = ref + rv
+    e, e2 = rel_err(y.float().cpu(), ref), rel_err(y.float().cpu(), y2.float().cpu())
+    print(f"halo upsample conv {n}x{H}x{W} {Cin}->{N}: rel vs fp32 {e:.2e}, vs tiled gather {e2:.2e}")
+    assert y.shape == (n, 2 * H, 2 * W, N) and e < 1e-2 and e2 < 1e-2
+    tot = lambda c: c.view(n, -1, 2, N).double().sum(1)
+    assert torch.allclose(tot(cs), tot(y2.gn_cs), rtol=2e-3, atol=1e-2 * 4 * H * W)
