@@ -428,7 +428,9 @@ int ls_add_rows(const uint16_t* x, int64_t rows, int32_t C, int32_t ldx, const f
  * patches, two blocks per CU, for Cin <= 256 (default on; off: 16 x 16, one block per CU);
  * key 17 = ls_ff_chain rows per wave: 1 = 16 rows (default), 2 = 32 rows, one wave per SIMD
  * (measured slower; diagnostics build only); key 18 = nearest-x2 upsample convs on the halo-tile
- * kernel (default on; off: the tiled gather). */
+ * kernel (default on; off: the tiled gather); key 19 = the narrow 16-column halo tile for 3x3 convs
+ * with N = 8 / 16 (the VAE's conv_out with conv_norm_out + SiLU fused; default on; off: the tiled
+ * 128 x 32 GEMM). */
 int ls_set_tuning(int32_t key, int32_t value);
 
 /* Diagnostics: workgroups per CU the runtime can co-schedule for a GEMM kernel

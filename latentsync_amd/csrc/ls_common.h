@@ -94,21 +94,18 @@ __device__ __forceinline__ float silu_log2(float u) {
   return u * __builtin_amdgcn_rcpf(fmaf(e, 1.4426950408889634f, 1.4426950408889634f));
 }
 
-// exact-erf GELU (diffusers GEGLU / whisper MLP) with a branch-free erf:
-// Abramowitz & Stegun 7.1.25, erf(z) = 1 - p(t) e^(-z^2), p(t) = a1 t + a2 t^2 + a3 t^3,
-// t = 1 / (1 + 0.47047 z), |erf error| <= 2.5e-5.  With z = |x| / sqrt(2) and
-// Phi(-a) = 1 - Phi(a) both signs are
-//   gelu(x) = x Phi(x) = relu(x) - |x| * (p(t) / 2) * e^(-x^2 / 2)
-// (p's coefficients halved): 11 VALU ops incl. one v_rcp_f32 and one v_exp_f32 (the 5-term
-// 7.1.26 form took 13), GELU abs error < 2.6e-5 on [-12, 12] against the fp64 erf form --
-// a twentieth of a bf16 ulp at the GELU's largest negative output (|y| = 0.17); the GEGLU
-// epilogues it sits in are VALU-issue-bound.
+// exact-erf GELU (diffusers GEGLU / whisper MLP), branch-free, as x * sigmoid(s(x)) with
+// s(x) = x (a + b x^2 + c x^4): (a, b, c) fitted minimax to the fp64 erf GELU, x^2 clamped
+// at 36 (beyond |x| = 6 the sigmoid is saturated either way and the quartic would turn
+// over).  Abs error 2.6e-5 on all of R in fp32 -- the accuracy of the Abramowitz & Stegun
+// 7.1.25 erf form this replaces (a twentieth of a bf16 ulp at the GELU's largest negative
+// output, |y| = 0.17) -- in 7 VALU ops + v_exp_f32 + v_rcp_f32 instead of 10 + the same two
+// (round 6: the GEGLU epilogues and the FeedForward kernels are VALU-issue-bound).  log2(e)
+// and the sign are folded into the coefficients: e = 2^(x t) = e^(-s(x)).
 __device__ __forceinline__ float gelu_erf(float x) {
-  const float ax = fabsf(x);
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.47047f * 0.70710678118654752f, ax, 1.0f));
-  const float hp = t * fmaf(t, fmaf(t, 0.3739278f, -0.0479399f), 0.1740121f);
-  const float e = fast_exp2(x * x * -0.72134752044448170f);
-  return fmaf(-ax, hp * e, fmaxf(x, 0.0f));
+  const float x2 = fminf(x * x, 36.0f);
+  const float t = fmaf(x2, fmaf(x2, 0.001014263f, -0.10677572f), -2.3011212f);
+  return x * __builtin_amdgcn_rcpf(1.0f + fast_exp2(x * t));
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

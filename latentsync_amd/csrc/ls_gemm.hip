@@ -2230,7 +2230,10 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
 template <int TW, int BN, int TH_ = 256 / TW>
 struct HaloCfg {
   static constexpr int TH = TH_;
-  static constexpr int NT = (TH / 4) * 2 * 64;           // threads: (TH / 4) pixel waves x 2 channel waves
+  // channel waves: 2 (BN / 2 columns each); 1 for the narrow tile (BN 16: the VAE decoder's
+  // conv_out, 3 used output channels, where the conv is bound by the halo transform and HBM)
+  static constexpr int WNW = BN >= 64 ? 2 : 1;
+  static constexpr int NT = (TH / 4) * WNW * 64;         // threads: (TH / 4) pixel waves x WNW channel waves
   static constexpr bool COMPACT = TH < 16;
   static constexpr int P = COMPACT ? TW + 2 : TW + 8;    // halo row pitch (pixels); padded: 0 mod 8
   static constexpr int HALO = (TH + 2) * P * 8;          // uint4 per halo image
@@ -2238,11 +2241,13 @@ struct HaloCfg {
   // weight ring slots (3 at BN 160 spills 30 VGPRs; the 2-block form has LDS for 2)
   static constexpr int NSW = COMPACT ? 2 : BN <= 128 ? 3 : 2;
   static constexpr int DPT = (WSLOT + NT - 1) / NT;      // weight DMAs per thread per tap
-  static constexpr int FN = BN / 32;                     // 16-column fragments per wave
+  static constexpr int FN = BN / WNW / 16;               // 16-column fragments per wave
   static constexpr size_t SHM = ((size_t)2 * HALO + (size_t)NSW * WSLOT + 64 + 64) * 16;  // + dummy, affine
   static_assert(SHM <= (COMPACT ? 81920 : 163840), "halo conv LDS (compact: two blocks per CU)");
   static_assert((size_t)64 * (BN + 4) * 4 <= (size_t)2 * HALO * 16, "epilogue staging fits the halo images");
   static_assert(TW == 16 && (TH == 16 || TH == 8), "16-pixel patch rows, 16 or 8 of them");
+  static_assert(BN % (16 * WNW) == 0, "whole 16-column fragments per wave");
+  static constexpr int MINB = BN >= 64 ? 16 / TH : 2;    // launch bounds: blocks per CU
 };
 
 
@@ -2260,13 +2265,13 @@ __host__ __device__ constexpr int halo_issue(int t, int nhl, bool gn) {
 // Halo pieces: the (TH + 2) x (TW + 2) pixels the taps read x 8 16-B chunks (2592 pieces at
 // 16 x 16: 5.06 per thread); piece j of a thread has its own LDS slot hdst[j].
 template <int TW, int BN, bool GN, bool CSF, int TH_ = 256 / TW>
-__global__ void __launch_bounds__(TH_ / 4 * 128, 16 / TH_) conv3x3_halo_kernel(ConvArgs a) {
+__global__ void __launch_bounds__((HaloCfg<TW, BN, TH_>::NT), (HaloCfg<TW, BN, TH_>::MINB)) conv3x3_halo_kernel(ConvArgs a) {
   using HC = HaloCfg<TW, BN, TH_>;
   constexpr int TH = HC::TH, P = HC::P, HALO = HC::HALO, WSLOT = HC::WSLOT, NSW = HC::NSW, NT = HC::NT;
+  constexpr int WNW = HC::WNW;
   constexpr bool COMPACT = HC::COMPACT;
-  static_assert(NT == TH_ / 4 * 128, "launch bounds");
   constexpr int NPC = (TH + 2) * (TW + 2) * 8;  // pieces per chunk (the read pixels)
-  constexpr int NHL = (NPC + NT - 1) / NT, DPT = HC::DPT, FM = 4, FN = HC::FN, WTN = BN / 2;
+  constexpr int NHL = (NPC + NT - 1) / NT, DPT = HC::DPT, FM = 4, FN = HC::FN, WTN = BN / WNW;
   constexpr int HB = (NHL + 2) / 3;  // largest batch
   extern __shared__ __attribute__((aligned(16))) uint4 lds_dyn[];
   uint4* const hbuf = lds_dyn;                 // [2][HALO]
@@ -2275,9 +2280,9 @@ __global__ void __launch_bounds__(TH_ / 4 * 128, 16 / TH_) conv3x3_halo_kernel(C
   float4* const gpar = (float4*)(dummy + 64);  // [2 chunk parities][scale 16 | shift 16] float4
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WNW, wn = wid % WNW;
   const int l16 = lane & 15, lg = lane >> 4;
-  const int ntn = a.N / BN, tpr = a.W / TW, tpc = a.H / TH;
+  const int ntn = (a.N + BN - 1) / BN, tpr = a.W / TW, tpc = a.H / TH;
   int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int tn = bid % ntn;
   bid /= ntn;
@@ -2375,7 +2380,8 @@ __global__ void __launch_bounds__(TH_ / 4 * 128, 16 / TH_) conv3x3_halo_kernel(C
   // ---- weight DMA: tap g = 9 ci + t is K-tile g of the channel-chunk-major packing
   // (buffer-descriptor DMA from column n0: per thread one byte offset, per tap the uniform
   // soffset g * 128 -- no 64-bit address arithmetic in the tap loop)
-  const i32x4 rs_w = buffer_rsrc(a.w + (long)n0 * a.K, (uint32_t)min((long)BN * a.K * 2, (long)cap));
+  // (rows n0 + BN > N -- the narrow tile over N = 8 -- lie past the descriptor and read zeros)
+  const i32x4 rs_w = buffer_rsrc(a.w + (long)n0 * a.K, (uint32_t)min((long)min(BN, a.N - n0) * a.K * 2, (long)cap));
   int wvo[DPT];
 #pragma unroll
   for (int j = 0; j < DPT; ++j) {
@@ -2494,7 +2500,7 @@ __global__ void __launch_bounds__(TH_ / 4 * 128, 16 / TH_) conv3x3_halo_kernel(C
   // epilogue: virtual rows (GroupNorm slots) = the patch's index within its image x 256
   const int m0v = (int)(img * HW) + (tyb * tpr + txb) * (TH * TW);
   const long m0r = img * HW + (long)y0 * a.W + x0;
-  store_tile_plain<TH * TW, BN, TH / 4, 2, false, CSF, TW>(a, acc, (float*)lds_dyn, m0v, n0, m0r);
+  store_tile_plain<TH * TW, BN, TH / 4, WNW, false, CSF, TW>(a, acc, (float*)lds_dyn, m0v, n0, m0r);
 }
 
 // ---------------------------------------------------------------- host side
@@ -2830,6 +2836,9 @@ static bool g_halo_ups = ls_env("LS_HALO_UPS") == nullptr || atoi(ls_env("LS_HAL
 // instead of 2 at BN 160)
 static bool g_halo_bn128 = ls_env("LS_HALO_BN128") != nullptr;
 
+// the narrow 16-column tile for N <= 16 (tuning key 19; off: the tiled GEMM's 128 x 32 tile)
+static bool g_halo_narrow = true;
+
 // patch width of the halo conv for this call (0: not taken)
 static int halo_tw(const ls_conv_desc* d, const ConvArgs& a) {
   if (!g_halo || g_force_tile || g_force_regstage || d->ksize != 3 || a.stride != 1 || a.pad != 1 ||
@@ -2843,7 +2852,9 @@ static int halo_tw(const ls_conv_desc* d, const ConvArgs& a) {
   // N <= 640: with more output channels the patch is re-loaded and re-transformed per N tile
   // and the tiled 256x256 kernel wins (VAE 512 channels at 32^2: 3667 vs 3409 us; 128 at
   // 256^2: 18660 vs 23610 us incl. the materialised GroupNorm; profiles/r04f_ab_t256_halo.txt)
-  if ((a.N % 160 && a.N % 128) || a.N > 640) return 0;
+  // (N = 8 / 16: the narrow tile -- conv_out of the VAE decoder / encoder, N padded to 8)
+  const bool narrow = a.N % 8 == 0 && a.N <= 16 && a.H % 8 == 0 && g_halo_narrow;
+  if (((a.N % 160 && a.N % 128) || a.N > 640) && !narrow) return 0;
   if (a.aff_scale && (!a.silu_in || a.pix_per_sample % (a.H * a.W) || ((uintptr_t)a.aff_scale | (uintptr_t)a.aff_shift) & 15))
     return 0;  // (the kernel's input transform is the GroupNorm affine + SiLU of a ResnetBlock)
   if (((uintptr_t)a.x1 | (uintptr_t)a.x2 | (uintptr_t)a.w) & 15 || a.ld1 % 8 || (a.C2 && a.ld2 % 8)) return 0;
@@ -2859,7 +2870,7 @@ static int halo_tw(const ls_conv_desc* d, const ConvArgs& a) {
 template <int TW, int BN, bool GN, bool CSF, int TH>
 static void launch_halo3(const ConvArgs& a, hipStream_t s) {
   using HC = HaloCfg<TW, BN, TH>;
-  const int grid = a.n_img * (a.H / HC::TH) * (a.W / TW) * (a.N / BN);
+  const int grid = a.n_img * (a.H / HC::TH) * (a.W / TW) * ((a.N + BN - 1) / BN);
   LS_SET_MAX_DYN_SHM((conv3x3_halo_kernel<TW, BN, GN, CSF, TH>), HC::SHM);
   conv3x3_halo_kernel<TW, BN, GN, CSF, TH><<<grid, HC::NT, HC::SHM, s>>>(a);
 }
@@ -2884,7 +2895,8 @@ static bool g_halo_th8 = ls_env("LS_HALO_TH8") == nullptr || atoi(ls_env("LS_HAL
 
 template <int TW>
 static void launch_halo1(const ConvArgs& a, hipStream_t s) {
-  if (a.N % 160 == 0 && !(g_halo_bn128 && a.N % 128 == 0)) launch_halo2<TW, 160>(a, s);
+  if (a.N <= 16) launch_halo2<TW, 16, 8>(a, s);
+  else if (a.N % 160 == 0 && !(g_halo_bn128 && a.N % 128 == 0)) launch_halo2<TW, 160>(a, s);
   else if (g_halo_th8 && a.H % 8 == 0 && a.Cin <= 256) launch_halo2<TW, 128, 8>(a, s);
   else launch_halo2<TW, 128>(a, s);
 }
@@ -2993,6 +3005,7 @@ extern int g_ff_chain_fmr;  // ls_ff.hip
 extern "C" int ls_set_tuning(int32_t key, int32_t value) {
   switch (key) {
     case 18: g_halo_ups = value != 0; return LS_OK;
+    case 19: g_halo_narrow = value != 0; return LS_OK;
     case 17:
 #ifndef LS_DIAG_KERNELS
       if (value == 2) return fail(LS_ERR_INVALID, "ls_ff_chain at 32 rows per wave: diagnostics build only");

@@ -104,7 +104,8 @@ class _DeviceVAE:
                            f"decoder.up_blocks.{i}.upsamplers.0.conv.bias") if i < len(boc) - 1 else None
             self.dec.append((res, us))
         self.dec_norm = (dv.f32("decoder.conv_norm_out.weight"), dv.f32("decoder.conv_norm_out.bias"))
-        self.dec_out = dv.packed("decoder.conv_out.weight", "decoder.conv_out.bias", n_pad=4)
+        # 8 output columns (3 used): the narrow halo-tile conv stores 16-B rows
+        self.dec_out = dv.packed("decoder.conv_out.weight", "decoder.conv_out.bias", n_pad=8)
 
     def encode_moments(self, x):
         """x NHWC bf16 (n, R, R, 8) (3 used channels) -> moments fp32 (n, R/8, R/8, 8)."""
@@ -119,11 +120,13 @@ class _DeviceVAE:
         for blk in self.enc_mid:
             h = blk(h)
         s = ops.group_norm(h, 32, 1e-6, *self.enc_norm, h.shape[0])
-        h = ops.conv(ops.group_norm_apply(h, s[0], s[1], h.shape[0], True), self.enc_out)
+        # conv_norm_out + SiLU fused into conv_out's halo transform (the narrow halo tile)
+        h = ops.conv(h, self.enc_out, aff=(s[0], s[1], 1, True), aff_materialize=True)
         return ops.conv(h, self.quant, out_f32=True)
 
     def decode(self, z):
-        """z NHWC bf16 (n, h, w, 8) (4 used channels, already / scaling) -> (n, 8h, 8w, 4) bf16."""
+        """z NHWC bf16 (n, h, w, 8) (4 used channels, already / scaling) -> (n, 8h, 8w, 8) bf16
+        (3 used channels)."""
         h = ops.conv(z, self.post_quant)
         h = ops.conv(h, self.dec_in, gn_out=True)
         for blk in self.dec_mid:
@@ -134,7 +137,7 @@ class _DeviceVAE:
             if us is not None:
                 h = ops.conv(h, us, upsample=True, gn_out=True)
         s = ops.group_norm(h, 32, 1e-6, *self.dec_norm, h.shape[0])
-        return ops.conv(ops.group_norm_apply(h, s[0], s[1], h.shape[0], True), self.dec_out)
+        return ops.conv(h, self.dec_out, aff=(s[0], s[1], 1, True), aff_materialize=True)
 
 
 class DiagonalGaussianDistribution:

@@ -154,3 +154,51 @@ def test_halo_conv_upsample(gpu, n, H, W, Cin, N, res):
     assert y.shape == (n, 2 * H, 2 * W, N) and e < 1e-2 and e2 < 1e-2
     tot = lambda c: c.view(n, -1, 2, N).double().sum(1)
     assert torch.allclose(tot(cs), tot(y2.gn_cs), rtol=2e-3, atol=1e-2 * 4 * H * W)
+
+
+@pytest.mark.parametrize("n,H,W,Cin,N,n_real,res", [
+    (2, 256, 256, 128, 8, 3, False),  # the VAE decoder's conv_out: 3 RGB channels padded to 8
+    (4, 32, 32, 512, 8, 8, False),    # the encoder's conv_out (2 x 4 latent moments)
+    (3, 32, 48, 64, 16, 16, True),    # 16 columns, one chunk, residual, non-square
+])
+def test_halo_conv_narrow(gpu, n, H, W, Cin, N, n_real, res):
+    """The narrow 16-column halo tile (N <= 16, tuning key 19): one channel wave, 16 x 8 patches,
+    weight rows past N read as zeros (buffer descriptor bound), with the GroupNorm affine + SiLU
+    of conv_norm_out fused (diffusers Decoder / Encoder: conv_out(silu(conv_norm_out(h)))).
+    Against fp32 and the tiled 128 x 32 GEMM on the materialised input, with column sums."""
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(n * 10 + H + Cin + N)
+    x = _bf(torch.randn(n, H, W, Cin, generator=g) * 2 + 0.5)
+    w = torch.zeros(N, Cin, 3, 3)
+    w[:n_real] = torch.randn(n_real, Cin, 3, 3, generator=g) / (9 * Cin) ** 0.5
+    b = torch.zeros(N)
+    b[:n_real] = 0.1 * torch.randn(n_real, generator=g)
+    scale = (1 + 0.2 * torch.randn(n, Cin, generator=g)).float()
+    shift = (0.3 * torch.randn(n, Cin, generator=g)).float()
+    rv = _bf(torch.randn(n, H, W, N, generator=g)) if res else None
+    pw = ops.Packed(pack_weight(w).to(torch.bfloat16).to(DEV), b.to(DEV), Cin, 3, N)
+    xd = x.to(torch.bfloat16).to(DEV)
+    kw = dict(aff=(scale.to(DEV), shift.to(DEV), 1, True))
+    if res:
+        kw["res"] = rv.to(torch.bfloat16).to(DEV)
+    assert ops.conv_path(xd, pw, **kw) == 3
+    y = ops.conv(xd, pw, gn_out=True, **kw)
+    cs = y.gn_cs.clone()
+    assert lib.ls_set_tuning(19, 0) == 0
+    try:
+        assert ops.conv_path(xd, pw, **kw) != 3
+        y2 = ops.conv(xd, pw, gn_out=True, aff_materialize=True, **kw)
+    finally:
+        lib.ls_set_tuning(19, 1)
+    xin = _bf(F.silu(x * scale[:, None, None, :] + shift[:, None, None, :]))
+    ref = F.conv2d(xin.permute(0, 3, 1, 2), w, b, padding=1).permute(0, 2, 3, 1)
+    if res:
+        ref = ref + rv
+    yc = y.float().cpu()
+    e, e2 = rel_err(yc, ref), rel_err(yc, y2.float().cpu())
+    print(f"narrow halo conv {n}x{H}x{W} {Cin}->{N} ({n_real} used): rel vs fp32 {e:.2e}, vs tiled {e2:.2e}")
+    assert y.shape == (n, H, W, N) and e < 1e-2 and e2 < 1e-2
+    if not res and n_real < N:  # the padded columns are exact zeros
+        assert yc[..., n_real:].abs().max().item() == 0.0
+    tot = lambda c: c.view(n, -1, 2, N).double().sum(1)
+    assert torch.allclose(tot(cs), tot(y2.gn_cs), rtol=2e-3, atol=1e-2 * H * W)
