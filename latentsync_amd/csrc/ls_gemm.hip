@@ -2390,15 +2390,23 @@ __global__ void __launch_bounds__((HaloCfg<TW, BN, TH_>::NT), (HaloCfg<TW, BN, T
     wvo[j] = ((q < WSLOT ? row : 0) * a.K + lc * 8) * 2;
   }
   // ring slot of tap g: with 3 slots, (9 ci + t) % 3 == t % 3 is known per tap at compile time
-  auto wslot = [&](int g, int t) { return NSW == 3 ? t % 3 : g % NSW; };
+  // (2 slots: (9 ci + t) % 2 == (ci + t) % 2, so with the chunk parity par = ci & 1 computed
+  // once per chunk the slot of every tap is one of two per-chunk values -- no per-tap g % 2)
+  auto wslot = [&](int par, int t) { return NSW == 3 ? t % 3 : (t & 1) ^ par; };
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+  __builtin_assume(wid_u >= 0 && wid_u < NT / 64);
+  // (LDS destinations as 32-bit LDS-space addresses: a generic-pointer select cast to LDS
+  // costs a null check per DMA, and with WSLOT % NT == 0 no DMA is a padding one)
+  typedef __attribute__((address_space(3))) uint4 lds_u4;
+  lds_u4* const wbuf_l = (lds_u4*)lds_dyn + 2 * HALO;
+  lds_u4* const dummy_l = wbuf_l + NSW * WSLOT;
   auto issue_w = [&](int g, int sl) {
-    uint4* slot = wbuf + sl * WSLOT;
+    lds_u4* slot = wbuf_l + sl * WSLOT + wid_u * 64;
 #pragma unroll
     for (int j = 0; j < DPT; ++j) {
-      const bool live = j * NT + wid_u * 64 < WSLOT;  // wave-uniform
-      ls_raw_buffer_load_lds(rs_w, (__attribute__((address_space(3))) void*)(live ? slot + j * NT + wid_u * 64 : dummy),
-                             16, wvo[j], g * 128, 0, 0);
+      const bool live = WSLOT % NT == 0 || j * NT + wid_u * 64 < WSLOT;  // wave-uniform
+      ls_raw_buffer_load_lds(rs_w, (__attribute__((address_space(3))) void*)(live ? slot + j * NT : dummy_l), 16, wvo[j],
+                             g * 128, 0, 0);
     }
   };
 
@@ -2441,7 +2449,7 @@ __global__ void __launch_bounds__((HaloCfg<TW, BN, TH_>::NT), (HaloCfg<TW, BN, T
         apf[ks][i] = __builtin_bit_cast(bf16x8, hb[base + 8 * (((16 * i) / TW) * P + (16 * i) % TW)]);
     }
   };
-  auto tap = [&](int ci, auto t_tag, auto last_tag) {
+  auto tap = [&](int ci, int par, auto t_tag, auto last_tag) {
     constexpr int t = decltype(t_tag)::value;
     constexpr bool LAST = decltype(last_tag)::value;  // no next chunk
     const int g = 9 * ci + t;
@@ -2454,14 +2462,14 @@ __global__ void __launch_bounds__((HaloCfg<TW, BN, TH_>::NT), (HaloCfg<TW, BN, T
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (g + NSW - 1 < G) issue_w(g + NSW - 1, wslot(g + NSW - 1, t + NSW - 1));
+    if (g + NSW - 1 < G) issue_w(g + NSW - 1, wslot(par, t + NSW - 1));
     if constexpr (!LAST) {
       if constexpr (GN && t == 1) store_par(ci + 1);  // read at taps 3 / 6 / 8, past a barrier
-      if constexpr (t == 3 || t == 6) store_halo((ci + 1) & 1, t / 3 - 1);
+      if constexpr (t == 3 || t == 6) store_halo(par ^ 1, t / 3 - 1);
       if constexpr (t == 0 || t == 3 || t == 6) load_halo(ci + 1, t / 3);
     }
-    const uint4* hb = hbuf + (ci & 1) * HALO;
-    const uint4* wb = wbuf + wslot(g, t) * WSLOT;
+    const uint4* hb = hbuf + par * HALO;
+    const uint4* wb = wbuf + wslot(par, t) * WSLOT;
     // A fragments of tap t: at t = 0 read here; for t > 0 read at the end of tap t - 1 (the
     // halo image is stable within a chunk), so after this tap's barrier only the weight
     // fragments stand between the wave and its MFMAs, and the LDS array serves 10 reads per
@@ -2480,7 +2488,7 @@ __global__ void __launch_bounds__((HaloCfg<TW, BN, TH_>::NT), (HaloCfg<TW, BN, T
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(apf[ks][i], bfr[j], acc[i][j], 0, 0, 0);
     }
     if constexpr (t < 8) read_a(hb, t + 1);
-    if constexpr (!LAST && t == 8) store_halo((ci + 1) & 1, 2);
+    if constexpr (!LAST && t == 8) store_halo(par ^ 1, 2);
   };
   using I0 = std::integral_constant<int, 0>; using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>; using I3 = std::integral_constant<int, 3>;
@@ -2488,9 +2496,10 @@ __global__ void __launch_bounds__((HaloCfg<TW, BN, TH_>::NT), (HaloCfg<TW, BN, T
   using I6 = std::integral_constant<int, 6>; using I7 = std::integral_constant<int, 7>;
   using I8 = std::integral_constant<int, 8>;
   auto chunk = [&](int ci, auto last) {
-    tap(ci, I0{}, last); tap(ci, I1{}, last); tap(ci, I2{}, last);
-    tap(ci, I3{}, last); tap(ci, I4{}, last); tap(ci, I5{}, last);
-    tap(ci, I6{}, last); tap(ci, I7{}, last); tap(ci, I8{}, last);
+    const int par = ci & 1;
+    tap(ci, par, I0{}, last); tap(ci, par, I1{}, last); tap(ci, par, I2{}, last);
+    tap(ci, par, I3{}, last); tap(ci, par, I4{}, last); tap(ci, par, I5{}, last);
+    tap(ci, par, I6{}, last); tap(ci, par, I7{}, last); tap(ci, par, I8{}, last);
   };
   for (int ci = 0; ci + 1 < nchunk; ++ci) chunk(ci, std::false_type{});
   chunk(nchunk - 1, std::true_type{});
