@@ -40,6 +40,9 @@ __device__ __forceinline__ i32x4 buffer_rsrc(const void* base, uint32_t bytes) {
   return r;
 }
 typedef uint16_t u16;
+// a 16-B LDS slot as an LDS-space (32-bit) pointer: LDS-DMA destinations computed in this
+// space need no generic -> LDS null check per instruction
+typedef __attribute__((address_space(3))) uint4 lds_u4;
 
 namespace ls {
 

@@ -271,23 +271,45 @@ __global__ void __launch_bounds__(512 / FMR, 1) ff_chain_kernel(FFChainArgs a) {
 
   for (int i = tid; i < 2 * I / 4; i += NT) ((float4*)b1s)[i] = ((const float4*)a.b1)[i];
 
-  // chunk g of the launch: [0, NA) Wo stages, [NA, NA + NCH) FeedForward chunks, then Wp stages
+  // chunk g of the launch: [0, NA) Wo stages, [NA, NA + NCH) FeedForward chunks, then Wp stages.
+  // Buffer-descriptor DMA: every per-thread byte offset is fixed over the chunks (W1 piece p:
+  // row (q >> 3) & 63 of the chunk, image q >> 9, swizzled chunk; W2 / Wo / Wp: slot u of the
+  // image), a chunk only moves the uniform soffset, and the LDS destinations are LDS-space
+  // addresses (one s_add to M0 per DMA instead of a 64-bit global address + readfirstlane).
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+  __builtin_assume(wid_u >= 0 && wid_u < NW);
+  const i32x4 rs_w1 = buffer_rsrc(a.w1, (uint32_t)(2L * I * C * 2));
+  const i32x4 rs_w2 = buffer_rsrc(a.w2, (uint32_t)((long)I * C * 2));
+  const i32x4 rs_wo = buffer_rsrc(a.wo, (uint32_t)((long)C * C * 2));
+  const i32x4 rs_wp = buffer_rsrc(a.wp, (uint32_t)((long)C * C * 2));
+  int vo1[PW1];
+#pragma unroll
+  for (int p = 0; p < PW1; ++p) {  // piece q: image q >> 9, row (q >> 3) & 63, physical chunk q & 7
+    const int q = p * NT + tid, r = (q >> 3) & 63, pc = q & 7;
+    const int lc = pc ^ ((r >> 1) & 7);
+    vo1[p] = (r * C + (q >> 9) * 64 + lc * 8) * 2;
+  }
+  const int vol = (wid_u * 64 + lane) * 16;  // slot u = wid + k NW of a [C][32] image: vol + k NW 1 KB
+  lds_u4* const lbase = (lds_u4*)lds;
   auto issue = [&](int g, int st) __attribute__((always_inline)) {
-    uint4* dst = lds + st * STAGE;
+    lds_u4* const dst = lbase + st * STAGE;
     if (g < NA || g >= NA + NCH) {
-      const int q = g < NA ? g : g - NA - NCH;
+      const bool o = g < NA;
+      const int q = o ? g : g - NA - NCH;
       const int nk = min(KPS, KT - q * KPS);
-      const u16* src = (g < NA ? a.wo : a.wp) + (long)q * KPS * W2IMG * 8;
-      for (int u = wid; u < nk * UW2; u += NW) glds16(src + ((long)u * 64 + lane) * 8, dst + u * 64);
+      const int so = q * KPS * W2IMG * 16;
+      for (int k = 0; wid_u + k * NW < nk * UW2; ++k)
+        ls_raw_buffer_load_lds(o ? rs_wo : rs_wp, (__attribute__((address_space(3))) void*)(dst + (wid_u + k * NW) * 64),
+                               16, vol + k * NW * 1024, so, 0, 0);
     } else {
       const int c = g - NA;
 #pragma unroll
-      for (int p = 0; p < PW1; ++p) {  // piece q: image q >> 9, row (q >> 3) & 63, physical chunk q & 7
-        const int q = p * NT + tid, r = (q >> 3) & 63, pc = q & 7;
-        const int lc = pc ^ ((r >> 1) & 7);
-        glds16(a.w1 + (long)(c * 64 + r) * C + (q >> 9) * 64 + lc * 8, dst + p * NT + wid * 64);
-      }
-      for (int u = wid; u < UW2; u += NW) glds16(a.w2 + ((long)c * W2IMG + u * 64 + lane) * 8, dst + WIMG + u * 64);
+      for (int p = 0; p < PW1; ++p)
+        ls_raw_buffer_load_lds(rs_w1, (__attribute__((address_space(3))) void*)(dst + p * NT + wid_u * 64), 16, vo1[p],
+                               c * 64 * C * 2, 0, 0);
+      for (int k = 0; wid_u + k * NW < UW2; ++k)
+        ls_raw_buffer_load_lds(rs_w2, (__attribute__((address_space(3))) void*)(dst + WIMG + (wid_u + k * NW) * 64), 16,
+                               vol + k * NW * 1024, c * W2IMG * 16, 0, 0);
     }
   };
   auto top = [&](int g) __attribute__((always_inline)) {  // chunk g's DMA landed everywhere; refill the other stage
@@ -520,7 +542,11 @@ __global__ void __launch_bounds__(512 / FMR, 1) ff_chain_kernel(FFChainArgs a) {
   } else {
     for (int c = 0; c < NCH; ++c) {
       const uint4* cur = top(NA + c);
+      // (the GEGLU biases are added after GEMM1: loaded into the accumulators before it, their
+      // LDS latency stood in front of the first MFMA -- 2623-2644 vs 2950-2970 us per call,
+      // profiles/r06n_chain_variants.txt)
       f32x4 acc[FMR][4];
+      const float* bb = b1s + c * 64 + 4 * lg;
   #pragma unroll
       for (int f = 0; f < FMR; ++f)
   #pragma unroll
@@ -554,18 +580,13 @@ __global__ void __launch_bounds__(512 / FMR, 1) ff_chain_kernel(FFChainArgs a) {
       }
   #pragma unroll
       for (int q = PD1; q < PD2; ++q) w2q[q] = w2[(q * 16 + l16) * 4 + p2];
-      const float* bb = b1s + c * 64 + 4 * lg;
-      const float4 bh0 = *(const float4*)(bb), bg0 = *(const float4*)(bb + 16);
-      const float4 bh1 = *(const float4*)(bb + 32), bg1 = *(const float4*)(bb + 48);
-      const float hb0[4] = {bh0.x, bh0.y, bh0.z, bh0.w}, gb0[4] = {bg0.x, bg0.y, bg0.z, bg0.w};
-      const float hb1[4] = {bh1.x, bh1.y, bh1.z, bh1.w}, gb1[4] = {bg1.x, bg1.y, bg1.z, bg1.w};
       bf16x8 gv[FMR];
   #pragma unroll
       for (int f = 0; f < FMR; ++f)
   #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          gv[f][r] = (__bf16)((acc[f][0][r] + hb0[r]) * gelu_erf(acc[f][1][r] + gb0[r]));
-          gv[f][4 + r] = (__bf16)((acc[f][2][r] + hb1[r]) * gelu_erf(acc[f][3][r] + gb1[r]));
+          gv[f][r] = (__bf16)((acc[f][0][r] + bb[r]) * gelu_erf(acc[f][1][r] + bb[16 + r]));
+          gv[f][4 + r] = (__bf16)((acc[f][2][r] + bb[32 + r]) * gelu_erf(acc[f][3][r] + bb[48 + r]));
         }
   #pragma unroll
       for (int t = 0; t < NT2; ++t) {

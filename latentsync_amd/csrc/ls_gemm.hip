@@ -1914,27 +1914,47 @@ __global__ void __launch_bounds__(512) gemm_rowblock_kernel(ConvArgs a) {
 #else
   constexpr int abl = 0;
 #endif
+  // W / residual DMA through buffer descriptors (round 6): the per-thread byte offsets are
+  // fixed over the chunks, a chunk moves only the uniform soffset, and the LDS destinations
+  // are LDS-space addresses -- one s_add to M0 per DMA instead of a 64-bit global address,
+  // a readfirstlane and the M0 copy (the same change took the ff_chain kernel 5-8 % faster)
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+  __builtin_assume(wid_u >= 0 && wid_u < 8);
+  const uint32_t cap = 0x7FFFFFFFu;
+  const i32x4 rs_w = buffer_rsrc(a.w, (uint32_t)min((long)a.N * a.K * 2, (long)cap));
+  const i32x4 rs_r = RES ? buffer_rsrc(a.res + (long)rb * BM * a.ldr, (uint32_t)min((long)BM * a.ldr * 2, (long)cap)) : rs_w;
+  int wvo[PPT], rvo[RPT > 0 ? RPT : 1];
+#pragma unroll
+  for (int p = 0; p < PPT; ++p) {
+    const int q = p * 512 + tid, t = q / (8 * BN), row = (q >> 3) % BN, pc = q & 7;
+    const int lc = pc ^ ((row >> 1) & 7);  // logical 16-B chunk stored at physical chunk pc
+    wvo[p] = (row * a.K + t * 64 + lc * 8) * 2;
+  }
+#pragma unroll
+  for (int p = 0; p < RPT; ++p) {  // residual piece q: row q / (BN / 8), 16-B column chunk q % (BN / 8)
+    const int q = p * 512 + tid, row = q / (BN / 8), ch = q % (BN / 8);
+    rvo[p] = (row * a.ldr + ch * 8) * 2;
+  }
+  lds_u4* const lbase = (lds_u4*)lds_dyn;
   auto issue = [&](int c, int stage) {
     if ((abl & 2) && c > c0 + 1) return;
-    uint4* dst = lds_dyn + stage * STAGE;
+    lds_u4* const dst = lbase + stage * STAGE;
 #pragma unroll
     for (int p = 0; p < PPT; ++p) {
-      const int q = p * 512 + tid, t = q / (8 * BN), row = (q >> 3) % BN, pc = q & 7;
-      const int lc = pc ^ ((row >> 1) & 7);  // logical 16-B chunk stored at physical chunk pc
-      if (WIMG % 512 == 0 || q < WIMG)       // (wave-uniform)
-        glds16(a.w + (long)(c * BN + row) * a.K + t * 64 + lc * 8, dst + p * 512 + wid * 64);
+      if (WIMG % 512 == 0 || p * 512 + wid_u * 64 < WIMG)  // (wave-uniform)
+        ls_raw_buffer_load_lds(rs_w, (__attribute__((address_space(3))) void*)(dst + p * 512 + wid_u * 64), 16, wvo[p],
+                               c * BN * a.K * 2, 0, 0);
     }
     if (wid == 0 && lane < 48 && (lane & 15) * 4 < BN) {
       const int q = lane >> 4, e = (lane & 15) * 4;
       const float* base = q == 0 ? a.bias : q == 1 ? nullptr : (RV ? a.rowvec + rv_base : nullptr);
       const void* ps = base ? (const void*)(base + c * BN + e) : (const void*)ls_zero_page;
-      glds16(ps, dst + WIMG);
+      glds16(ps, lds_dyn + stage * STAGE + WIMG);
     }
 #pragma unroll
-    for (int p = 0; p < RPT; ++p) {  // residual piece q: row q / (BN / 8), 16-B column chunk q % (BN / 8)
-      const int q = p * 512 + tid, row = q / (BN / 8), ch = q % (BN / 8);
-      glds16(a.res + (long)(rb * BM + row) * a.ldr + c * BN + ch * 8, dst + WIMG + 48 + p * 512 + wid * 64);
-    }
+    for (int p = 0; p < RPT; ++p)
+      ls_raw_buffer_load_lds(rs_r, (__attribute__((address_space(3))) void*)(dst + WIMG + 48 + p * 512 + wid_u * 64), 16,
+                             rvo[p], c * BN * 2, 0, 0);
   };
 
   if (c0 >= c1) return;
@@ -2397,7 +2417,6 @@ __global__ void __launch_bounds__((HaloCfg<TW, BN, TH_>::NT), (HaloCfg<TW, BN, T
   __builtin_assume(wid_u >= 0 && wid_u < NT / 64);
   // (LDS destinations as 32-bit LDS-space addresses: a generic-pointer select cast to LDS
   // costs a null check per DMA, and with WSLOT % NT == 0 no DMA is a padding one)
-  typedef __attribute__((address_space(3))) uint4 lds_u4;
   lds_u4* const wbuf_l = (lds_u4*)lds_dyn + 2 * HALO;
   lds_u4* const dummy_l = wbuf_l + NSW * WSLOT;
   auto issue_w = [&](int g, int sl) {

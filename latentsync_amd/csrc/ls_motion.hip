@@ -116,20 +116,31 @@ __global__ void __launch_bounds__(TCfg<C>::NT, TCfg<C>::MINB) tattn_fused_kernel
   // sub-chunk c (W rows [c BN, c BN + BN) x all C) -> stage: KT/2 64-wide swizzled images.
   // Every wave issues exactly DPW DMA instructions per stage (the spare ones re-fetch
   // row 0 into a dummy slot), so "stage c landed" is one constant vmcnt for all waves.
-  uint4* dummy = lds_w + T::NST * STAGE;
+  // (round 6) buffer-descriptor DMA: per-thread byte offsets fixed over the sub-chunks, the
+  // sub-chunk in the uniform soffset, LDS-space destinations, and the live / spare choice on
+  // the scalar wave index -- the generic-address form spent ~5 VALU / SALU per DMA on a 64-bit
+  // address, a readfirstlane for M0 and an exec-masked branch
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+  __builtin_assume(wid_u >= 0 && wid_u < T::WAVES);
+  const i32x4 rs_w = buffer_rsrc(a.w, (uint32_t)min(3L * C * C * 2, 0x7FFFFFFFL));
+  int wvo[T::DPW];
+#pragma unroll
+  for (int p = 0; p < T::DPW; ++p) {
+    const int u = p * T::WAVES + wid_u;  // wave-instruction index within the stage
+    const int q = u * 64 + lane, t = q / (8 * BN), row = (q >> 3) % BN, pc = q & 7;
+    const int lc = pc ^ ((row >> 1) & 7);
+    wvo[p] = (STAGE % (64 * T::WAVES) == 0 || u < STAGE / 64) ? (row * C + t * 64 + lc * 8) * 2 : lane * 16;
+  }
+  lds_u4* const lbase = (lds_u4*)lds_w;
+  lds_u4* const dummy_l = lbase + T::NST * STAGE;
   auto issue = [&](int c) {
-    uint4* dst = lds_w + (c % T::NST) * STAGE;
-    const u16* src = a.w + (long)c * BN * C;
+    lds_u4* const dst = lbase + (c % T::NST) * STAGE;
 #pragma unroll
     for (int p = 0; p < T::DPW; ++p) {
-      const int u = p * T::WAVES + wid;  // wave-instruction index within the stage (wave-uniform)
-      if (STAGE % (64 * T::WAVES) == 0 || u < STAGE / 64) {
-        const int q = u * 64 + lane, t = q / (8 * BN), row = (q >> 3) % BN, pc = q & 7;
-        const int lc = pc ^ ((row >> 1) & 7);
-        glds16(src + (long)row * C + t * 64 + lc * 8, dst + u * 64);
-      } else {
-        glds16(src + lane * 8, dummy);
-      }
+      const int u = p * T::WAVES + wid_u;  // (wave-uniform)
+      const bool live = STAGE % (64 * T::WAVES) == 0 || u < STAGE / 64;
+      ls_raw_buffer_load_lds(rs_w, (__attribute__((address_space(3))) void*)(live ? dst + u * 64 : dummy_l), 16, wvo[p],
+                             c * BN * C * 2, 0, 0);
     }
   };
 
