@@ -430,7 +430,8 @@ int ls_add_rows(const uint16_t* x, int64_t rows, int32_t C, int32_t ldx, const f
  * (measured slower; diagnostics build only); key 18 = nearest-x2 upsample convs on the halo-tile
  * kernel (default on; off: the tiled gather); key 19 = the narrow 16-column halo tile for 3x3 convs
  * with N = 8 / 16 (the VAE's conv_out with conv_norm_out + SiLU fused; default on; off: the tiled
- * 128 x 32 GEMM). */
+ * 128 x 32 GEMM); key 20 = the K = 640 residual linears on the row-block GEMM (default off: the
+ * tiled 128 x 160 kernel). */
 int ls_set_tuning(int32_t key, int32_t value);
 
 /* Diagnostics: workgroups per CU the runtime can co-schedule for a GEMM kernel

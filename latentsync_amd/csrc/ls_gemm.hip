@@ -2303,6 +2303,8 @@ __global__ void __launch_bounds__((HaloCfg<TW, BN, TH_>::NT), (HaloCfg<TW, BN, T
   const int wm = wid / WNW, wn = wid % WNW;
   const int l16 = lane & 15, lg = lane >> 4;
   const int ntn = (a.N + BN - 1) / BN, tpr = a.W / TW, tpc = a.H / TH;
+  // (measured, not kept: a persistent grid issuing the next tile's weights and halo loads
+  // before this tile's epilogue -- 30-90 VGPRs of spills in every instance)
   int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int tn = bid % ntn;
   bid /= ntn;
@@ -2331,19 +2333,27 @@ __global__ void __launch_bounds__((HaloCfg<TW, BN, TH_>::NT), (HaloCfg<TW, BN, T
   for (int j = 0; j < NHL; ++j) {
     const int q = j * NT + tid, hp = q >> 3;
     const int hr = hp / (TW + 2), hcol = hp - hr * (TW + 2);
-    const int y = y0 - 1 + hr, x = x0 - 1 + hcol;
     if constexpr (COMPACT) {  // row hr, column hcol, the chunk swizzled by the column
       hdst[j] = (hr * P + hcol) * 8 + (hc8 ^ (hcol & 7));
     } else {
       const int slot = hr * P + hcol + 3;
       hdst[j] = slot * 8 + (hc8 ^ (slot & 7));
     }
-    hpix[j] = q < NPC && y >= 0 && y < a.H && x >= 0 && x < a.W ? (y >> ups) * Wi + (x >> ups) : -1;
   }
   const uint32_t cap = 0x7FFFFFFFu;
+#pragma unroll
+  for (int j = 0; j < NHL; ++j) {
+    const int q = j * NT + tid, hp = q >> 3;
+    const int hr = hp / (TW + 2), hcol = hp - hr * (TW + 2);
+    const int y = y0 - 1 + hr, x = x0 - 1 + hcol;
+    hpix[j] = q < NPC && y >= 0 && y < a.H && x >= 0 && x < a.W ? (y >> ups) * Wi + (x >> ups) : -1;
+  }
   const i32x4 rs1 = buffer_rsrc(a.x1 + img * HWi * a.ld1, (uint32_t)min((long)HWi * a.ld1 * 2, (long)cap));
   const i32x4 rs2 = a.C2 ? buffer_rsrc(a.x2 + img * HWi * a.ld2, (uint32_t)min((long)HWi * a.ld2 * 2, (long)cap)) : rs1;
   const long aff0 = (long)img * HW / a.pix_per_sample * a.Cin;
+  // weight descriptor from column n0 (rows n0 + BN > N -- the narrow tile over N = 8 -- lie
+  // past it and read zeros)
+  const i32x4 rs_w = buffer_rsrc(a.w + (long)n0 * a.K, (uint32_t)min((long)min(BN, a.N - n0) * a.K * 2, (long)cap));
   uint4 hreg[HB];
   float4 gp;
   // the affine parameters of chunk ci (64 scales, 64 shifts): every thread loads one float4
@@ -2370,9 +2380,9 @@ __global__ void __launch_bounds__((HaloCfg<TW, BN, TH_>::NT), (HaloCfg<TW, BN, T
       if (b == 0 && ci > 0) load_par(ci);
     }
   };
-  auto store_halo = [&](int buf, int b) {
+  // pieces [j0, j1) of a chunk's halo image buf from v[j - j0] (+ the affine + SiLU)
+  auto put_halo = [&](int buf, int j0, int j1, const uint4* v_in) __attribute__((always_inline)) {
     uint4* const hb0 = hbuf + buf * HALO;
-    const int j0 = hb_lo(b, NHL), j1 = hb_lo(b + 1, NHL);
     float4 gsc[2], gsh[2];
     if constexpr (GN) {  // this thread's 8 channels (chunk parity buf)
       const float4* gq = gpar + buf * 32 + hc8 * 2;
@@ -2381,7 +2391,7 @@ __global__ void __launch_bounds__((HaloCfg<TW, BN, TH_>::NT), (HaloCfg<TW, BN, T
 #pragma unroll
     for (int j = j0; j < j1; ++j) {
       if (j * NT + tid >= NPC) continue;
-      uint4 v = hreg[j - j0];
+      uint4 v = v_in[j - j0];
       if constexpr (GN) {
         if (hpix[j] >= 0) {  // zero padding stays zero: the conv pads the ACTIVATED input
           float f[8];
@@ -2396,12 +2406,11 @@ __global__ void __launch_bounds__((HaloCfg<TW, BN, TH_>::NT), (HaloCfg<TW, BN, T
       hb0[hdst[j]] = v;
     }
   };
+  auto store_halo = [&](int buf, int b) { put_halo(buf, hb_lo(b, NHL), hb_lo(b + 1, NHL), hreg); };
 
   // ---- weight DMA: tap g = 9 ci + t is K-tile g of the channel-chunk-major packing
   // (buffer-descriptor DMA from column n0: per thread one byte offset, per tap the uniform
   // soffset g * 128 -- no 64-bit address arithmetic in the tap loop)
-  // (rows n0 + BN > N -- the narrow tile over N = 8 -- lie past the descriptor and read zeros)
-  const i32x4 rs_w = buffer_rsrc(a.w + (long)n0 * a.K, (uint32_t)min((long)min(BN, a.N - n0) * a.K * 2, (long)cap));
   int wvo[DPT];
 #pragma unroll
   for (int j = 0; j < DPT; ++j) {
@@ -2441,17 +2450,23 @@ __global__ void __launch_bounds__((HaloCfg<TW, BN, TH_>::NT), (HaloCfg<TW, BN, T
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  // prologue: weights of taps 0 .. NSW - 2, halo of chunk 0
+  // prologue: weights of taps 0 .. NSW - 2, the chunk-0 affine row, and every chunk-0 halo
+  // piece into registers at once (one HBM round trip, not one per batch), then the image
+  // (chunk 0 reads source 1: host C1 % 64 == 0, C1 > 0)
   for (int g = 0; g < NSW - 1 && g < G; ++g) issue_w(g, g % NSW);
-  if constexpr (GN) {
-    load_par(0);
-    store_par(0);
-    __syncthreads();
-  }
+  {
+    uint4 hpre[NHL];
+    if constexpr (GN) load_par(0);
 #pragma unroll
-  for (int b = 0; b < 3; ++b) {
-    load_halo(0, b);
-    store_halo(0, b);  // (the compiler waits for the loads)
+    for (int j = 0; j < NHL; ++j) {
+      const int vo = hpix[j] >= 0 ? hpix[j] * a.ld1 * 2 + hc8 * 16 : (int)0x80000000;
+      hpre[j] = __builtin_bit_cast(uint4, ls_raw_buffer_load_v4(rs1, vo, 0, 0));
+    }
+    if constexpr (GN) {
+      store_par(0);
+      __syncthreads();
+    }
+    put_halo(0, 0, NHL, hpre);  // (the compiler waits for the loads)
   }
 
   bf16x8 apf[2][FM];  // A fragments of the current tap (both k-steps)
@@ -2898,9 +2913,9 @@ static int halo_tw(const ls_conv_desc* d, const ConvArgs& a) {
 template <int TW, int BN, bool GN, bool CSF, int TH>
 static void launch_halo3(const ConvArgs& a, hipStream_t s) {
   using HC = HaloCfg<TW, BN, TH>;
-  const int grid = a.n_img * (a.H / HC::TH) * (a.W / TW) * ((a.N + BN - 1) / BN);
+  const int ntile = a.n_img * (a.H / HC::TH) * (a.W / TW) * ((a.N + BN - 1) / BN);
   LS_SET_MAX_DYN_SHM((conv3x3_halo_kernel<TW, BN, GN, CSF, TH>), HC::SHM);
-  conv3x3_halo_kernel<TW, BN, GN, CSF, TH><<<grid, HC::NT, HC::SHM, s>>>(a);
+  conv3x3_halo_kernel<TW, BN, GN, CSF, TH><<<ntile, HC::NT, HC::SHM, s>>>(a);
 }
 
 template <int TW, int BN, int TH = 256 / TW>
@@ -3034,6 +3049,7 @@ extern "C" int ls_set_tuning(int32_t key, int32_t value) {
   switch (key) {
     case 18: g_halo_ups = value != 0; return LS_OK;
     case 19: g_halo_narrow = value != 0; return LS_OK;
+    case 20: g_rb640_res = value != 0; return LS_OK;
     case 17:
 #ifndef LS_DIAG_KERNELS
       if (value == 2) return fail(LS_ERR_INVALID, "ls_ff_chain at 32 rows per wave: diagnostics build only");
