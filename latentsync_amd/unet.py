@@ -40,6 +40,9 @@ _FUSED_FF = _lib.ab_switch("LS_FUSED_FF", "1") != "0"
 # LS_FF_CHAIN=0: the 32x32-level block tail (to_out + LN + FeedForward + proj_out) as three
 # launches (row-block GEMM, ls_feedforward, row-block GEMM) instead of one ls_ff_chain
 _FF_CHAIN = _lib.ab_switch("LS_FF_CHAIN", "1") != "0"
+# conv_norm_out + SiLU + conv_out on the narrow halo tile, conv_out padded to 8 columns (round 6;
+# "0" in diagnostics mode: the materialised GroupNorm and the 4-column tiled GEMM)
+_NARROW_OUT = _lib.ab_switch("LS_NARROW_OUT", "1") != "0"
 # LS_FUSED_XATTN=1: the audio cross-attention branch at C = 320 as ONE ls_cross_attention_block
 # launch instead of q GEMM + ls_attention + out GEMM.  Off by default: measured 1-2 ms per
 # 48-window step SLOWER than the three launches (profiles/r04k_step_ab.txt)
@@ -407,7 +410,10 @@ class _DeviceUNet:
             self.up.append((layers, us))
         self.norm_out = (dv.f32("conv_norm_out.weight"), dv.f32("conv_norm_out.bias"))
         self.groups, self.eps = groups, eps
-        self.conv_out = dv.packed("conv_out.weight", "conv_out.bias")
+        # 8 output columns (out_channels used): the narrow halo-tile conv (N = 8 / 16) stores 16-B
+        # rows and takes conv_norm_out + SiLU in its halo transform
+        self.conv_out = dv.packed("conv_out.weight", "conv_out.bias",
+                                  n_pad=(self.cout + 7) // 8 * 8 if self.cout <= 16 and _NARROW_OUT else None)
         self.temb_w = torch.cat(temb_w, 0).to(torch.bfloat16).to(device).contiguous()
         self.temb_b = torch.cat(temb_b, 0).float().to(device).contiguous()
 
@@ -442,7 +448,8 @@ class _DeviceUNet:
 
     def forward(self, x_in, B, ts_i32, step_i32, audio_rows, n_audio_tok, down_res=None, mid_res=None,
                 audio_kv=None, t_rows=None):
-        """x_in NHWC bf16 (B*F, H, W, cin_pad) -> eps NHWC bf16 (B*F, H, W, out_channels).
+        """x_in NHWC bf16 (B*F, H, W, cin_pad) -> eps NHWC bf16 (B*F, H, W, n) with out_channels
+        used of n (8 for the UNet's 4: conv_out runs on the narrow halo tile).
         audio_kv: the dict of audio_kv(audio_rows), precomputed once per window batch.
         t_rows: fp32 timesteps (1 or B values) instead of ts_i32[step_i32]."""
         kvs = audio_kv or {}
@@ -480,7 +487,9 @@ class _DeviceUNet:
             if us is not None:
                 h = ops.conv(h, us, upsample=True, gn_out=True)
         sc = ops.group_norm(h, self.groups, self.eps, *self.norm_out, B)
-        return ops.conv(ops.group_norm_apply(h, sc[0], sc[1], B, True), self.conv_out)
+        if not _NARROW_OUT:
+            return ops.conv(ops.group_norm_apply(h, sc[0], sc[1], B, True), self.conv_out)
+        return ops.conv(h, self.conv_out, aff=(sc[0], sc[1], h.shape[0] // B, True), aff_materialize=True)
 
 
 # --------------------------------------------------------------------------
