@@ -293,7 +293,14 @@ __device__ __forceinline__ void epi_side_load(const ConvArgs& a, int m0, int n0,
 // (GroupNorm slots) and m0r the real first row.  PRE: pass 0's side inputs were loaded by
 // the caller (epi_side_load during its last K-tile) into `pre`.  Pass p + 1's side inputs
 // are issued right after pass p's staging barrier, so only the first pass waits on HBM.
-template <int BM, int BN, int WM, int WN, bool GEN, bool CSF = false, int RW = 0, bool PRE = false, bool PIPE = true>
+// CSG > 1 (round 6, the halo convs): the column sums are kept per thread in registers -- its
+// 8-column chunk summed over the rows it stores, across the passes of a 128-row slot -- and
+// only at the slot's end do the RPI threads of a chunk column meet through LDS (the staging
+// image; a fixed order).  The per-pass form wrote every stored value back to the staging image
+// and had BN threads re-read all WTM rows: 10-14 % of the 16x16 halo conv (scripts/cs_cost.py).
+// (The caller guarantees (NT / (BN / 8)) x BN x 2 floats of LDS at st.)
+template <int BM, int BN, int WM, int WN, bool GEN, bool CSF = false, int RW = 0, bool PRE = false, bool PIPE = true,
+          int CSG = 1>
 __device__ __forceinline__ void store_tile_plain_pre(const ConvArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
                                                      float* st, int m0, int n0, long m0r, int tid_in,
                                                      const EpiSide<EpiGeo<BM, BN, WM, WN>::ITER>& pre) {
@@ -311,6 +318,9 @@ __device__ __forceinline__ void store_tile_plain_pre(const ConvArgs& a, f32x4 (&
   const bool cok = (r0 < RPI) && col < a.N;
   const bool cs_on = CSOK && a.cs_out != nullptr;
   float g1 = 0.f, g2 = 0.f;  // column tid's sums over the slot's passes so far
+  float q1[8], q2[8];        // (CSG > 1) this thread's chunk sums over its stored rows of the slot
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { q1[j] = 0.f; q2[j] = 0.f; }
   // row vector (per-frame temb / positional-encoding rows): one row for the whole
   // tile in the common case (rows_per_vec >= the tile's row span), folded into
   // the per-column constants; otherwise looked up per row.
@@ -384,17 +394,46 @@ __device__ __forceinline__ void store_tile_plain_pre(const ConvArgs& a, f32x4 (&
       } else {
         const uint4 pk = pack8(v);
         *(uint4*)((u16*)a.y + (long)row * a.ldy + col) = pk;
-        if (cs_on) {  // the stored values replace their fp32 staging
+        if (cs_on) {
           float b[8];
           unpack8(pk, b);
-          float* sw = st + rl * SP + c8;
-          *(float4*)sw = make_float4(b[0], b[1], b[2], b[3]);
-          *(float4*)(sw + 4) = make_float4(b[4], b[5], b[6], b[7]);
+          if constexpr (CSG > 1) {  // sums of the stored (bf16) values, in registers
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { q1[j] += b[j]; q2[j] = fmaf(b[j], b[j], q2[j]); }
+          } else {  // the stored values replace their fp32 staging
+            float* sw = st + rl * SP + c8;
+            *(float4*)sw = make_float4(b[0], b[1], b[2], b[3]);
+            *(float4*)(sw + 4) = make_float4(b[4], b[5], b[6], b[7]);
+          }
         }
       }
     }
     __syncthreads();
-    if (cs_on) {  // (block-uniform)
+    if (cs_on && CSG > 1) {  // (block-uniform) the slot's end: the RPI chunk partials of a column meet
+      if (((p + 1) * WTM) % CS_ROWS == 0) {
+        float2* const part = (float2*)st;  // [RPI][BN] (sum, sum of squares)
+        if (cok) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) part[r0 * BN + c8 + j] = make_float2(q1[j], q2[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { q1[j] = 0.f; q2[j] = 0.f; }
+        __syncthreads();
+        if (tid < BN && n0 + tid < a.N) {
+          float t1 = 0.f, t2 = 0.f;
+#pragma unroll 5
+          for (int r = 0; r < RPI; ++r) {
+            const float2 v = part[r * BN + tid];
+            t1 += v.x;
+            t2 += v.y;
+          }
+          float* o = a.cs_out + (m0 + (long)p * WTM) / CS_ROWS * 2 * a.N + n0 + tid;
+          o[0] = t1;
+          o[a.N] = t2;
+        }
+        __syncthreads();  // the next pass stages into st
+      }
+    } else if (cs_on) {  // (block-uniform)
       const bool mine = tid < BN && n0 + tid < a.N;
       if (mine) {
         float t1 = 0.f, t2 = 0.f;
@@ -424,14 +463,14 @@ __device__ __forceinline__ void store_tile_plain_pre(const ConvArgs& a, f32x4 (&
   }
 }
 
-template <int BM, int BN, int WM, int WN, bool GEN, bool CSF = false, int RW = 0>
+template <int BM, int BN, int WM, int WN, bool GEN, bool CSF = false, int RW = 0, int CSG = 1>
 __device__ __forceinline__ void store_tile_plain(const ConvArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
                                                  float* st, int m0, int n0, long m0r = 0, int tid_in = -1) {
   // (the 8-wave 256 x 256 tile runs at the 256-VGPR limit: its next pass's residual loads
   // would spill, so they stay in the pass)
   EpiSide<EpiGeo<BM, BN, WM, WN>::ITER> none;
-  store_tile_plain_pre<BM, BN, WM, WN, GEN, CSF, RW, false, !(BM == 256 && WM == 2)>(a, acc, st, m0, n0, m0r, tid_in,
-                                                                                     none);
+  store_tile_plain_pre<BM, BN, WM, WN, GEN, CSF, RW, false, !(BM == 256 && WM == 2), CSG>(a, acc, st, m0, n0, m0r,
+                                                                                          tid_in, none);
 }
 
 // GEGLU variant: a thread owns one 8-wide OUTPUT chunk, i.e. packed columns
@@ -2543,7 +2582,9 @@ __global__ void __launch_bounds__((HaloCfg<TW, BN, TH_>::NT), (HaloCfg<TW, BN, T
   // epilogue: virtual rows (GroupNorm slots) = the patch's index within its image x 256
   const int m0v = (int)(img * HW) + (tyb * tpr + txb) * (TH * TW);
   const long m0r = img * HW + (long)y0 * a.W + x0;
-  store_tile_plain<TH * TW, BN, TH / 4, WNW, false, CSF, TW>(a, acc, (float*)lds_dyn, m0v, n0, m0r);
+  // column sums from per-thread register partials (CSG = 2: store_tile_plain_pre's slot-end form)
+  static_assert((size_t)(NT / (BN / 8)) * BN * 2 * 4 <= (size_t)2 * HALO * 16, "column-sum partials fit the halo images");
+  store_tile_plain<TH * TW, BN, TH / 4, WNW, false, CSF, TW, 2>(a, acc, (float*)lds_dyn, m0v, n0, m0r);
 }
 
 // ---------------------------------------------------------------- host side
