@@ -13,7 +13,10 @@ from latentsync_amd.packing import pack_weight  # noqa: E402
 dev = torch.device("cuda", 0)
 SHAPES = [("unet 32^2 320->320 aff", 768, 32, 320, 320, True), ("unet 16^2 640->640 aff", 768, 16, 640, 640, True),
           ("vae 256^2 128->128 aff", 96, 256, 128, 128, True), ("vae 128^2 256->256 aff", 192, 128, 256, 256, True),
-          ("unet 8^2 1280->1280 aff", 768, 8, 1280, 1280, True), ("unet 32^2 1x1 320->320", 768, 32, 320, 320, None)]
+          ("unet 8^2 1280->1280 aff", 768, 8, 1280, 1280, True), ("unet 32^2 1x1 320->320", 768, 32, 320, 320, None),
+          ("unet 16^2 1x1 640->640 +res", 768, 16, 640, 640, "res"),
+          ("unet 8^2 1x1 1280->1280 +res", 768, 8, 1280, 1280, "res")]
+SHAPES = [t for t in SHAPES if not os.environ.get("CS_ONLY") or any(o in t[0] for o in os.environ["CS_ONLY"].split(","))]
 
 
 def timed(fn, n=15):
@@ -31,12 +34,14 @@ def timed(fn, n=15):
 
 
 for name, n, H, cin, cout, aff in SHAPES:
-    ks = 1 if aff is None else 3
+    ks = 3 if aff is True else 1
     x = torch.randn(n, H, H, cin, device=dev).to(torch.bfloat16)
     w = torch.randn(cout, cin, ks, ks) / (cin * ks * ks) ** 0.5
     pw = ops.Packed(pack_weight(w).to(torch.bfloat16).to(dev), torch.zeros(cout, device=dev), cin, ks, cout)
     kw = {}
-    if aff:
+    if aff == "res":
+        kw = dict(res=torch.randn(n, H, H, cout, device=dev).to(torch.bfloat16))
+    elif aff:
         kw = dict(aff=(torch.rand(n, cin, device=dev) + 0.5, torch.randn(n, cin, device=dev) * 0.1, 1, True),
                   aff_materialize=True)
     out = torch.empty(n, H, H, cout, dtype=torch.bfloat16, device=dev)
