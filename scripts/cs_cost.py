@@ -1,5 +1,6 @@
 """Cost of the GroupNorm column sums in the conv epilogue: one conv shape timed with and without
-gn_out (the kernel's CSF instance vs the plain one), HIP events, median of 15 launches.
+gn_out (the kernel's CSF instance vs the plain one), HIP events, median of 15 launches, the two
+arms alternated three times (timing one arm first biased it: the chip had not reached its clock).
 usage: python scripts/cs_cost.py"""
 import os
 import sys
@@ -46,7 +47,13 @@ for name, n, H, cin, cout, aff in SHAPES:
                   aff_materialize=True)
     out = torch.empty(n, H, H, cout, dtype=torch.bfloat16, device=dev)
     path = ops.conv_path(x, pw, **{k: v for k, v in kw.items() if k == "aff"})
-    t1 = timed(lambda: ops.conv(x, pw, out=out, gn_out=True, **kw))
-    t0 = timed(lambda: ops.conv(x, pw, out=out, gn_out=False, **kw))
+    # alternated, three rounds each (the first-measured arm had run at a lower clock)
+    f1 = lambda: ops.conv(x, pw, out=out, gn_out=True, **kw)
+    f0 = lambda: ops.conv(x, pw, out=out, gn_out=False, **kw)
+    r1, r0 = [], []
+    for _ in range(3):
+        r0.append(timed(f0))
+        r1.append(timed(f1))
+    t1, t0 = sorted(r1)[1], sorted(r0)[1]
     print(f"{name:28s} path {path}: with column sums {t1:9.1f} us, without {t0:9.1f} us, cost {t1 - t0:+8.1f} us "
           f"({(t1 - t0) / t0 * 100:+.1f} %)")
